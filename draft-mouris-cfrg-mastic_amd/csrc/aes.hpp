@@ -1,0 +1,119 @@
+// AES-128 for XofFixedKeyAes128 (vdaf_poc.xof, vdaf-13) on gfx950.
+//
+// T-table AES with ONE table T0 in LDS, replicated 32 times so that lane l
+// always reads bank (l mod 32): random-index lookups are bank-conflict free
+// (ds_read_b32 services lanes in two groups of 32, one bank each).  The other
+// three tables are byte rotations of T0 (v_alignbit_b32).  32 KiB of LDS.
+//
+// State bytes are kept as four little-endian column words
+// (column c = bytes 4c..4c+3), matching the wire byte order of the block.
+#pragma once
+#include "common.hpp"
+
+#define AES_LDS_WORDS (256 * 32)
+
+static constexpr uint8_t AES_SBOX[256] = {
+    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76,
+    0xca, 0x82, 0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0,
+    0xb7, 0xfd, 0x93, 0x26, 0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15,
+    0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96, 0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75,
+    0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0, 0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84,
+    0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb, 0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf,
+    0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f, 0x50, 0x3c, 0x9f, 0xa8,
+    0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff, 0xf3, 0xd2,
+    0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
+    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb,
+    0xe0, 0x32, 0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79,
+    0xe7, 0xc8, 0x37, 0x6d, 0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08,
+    0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6, 0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a,
+    0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e, 0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e,
+    0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e, 0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf,
+    0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
+
+MH_HD uint32_t aes_xtime(uint32_t b) { return ((b << 1) ^ ((b & 0x80) ? 0x1b : 0)) & 0xff; }
+
+// T0[x] little-endian word = (2S, S, S, 3S)
+MH_HD uint32_t aes_t0(int x) {
+    uint32_t s = AES_SBOX[x];
+    uint32_t s2 = aes_xtime(s);
+    uint32_t s3 = s2 ^ s;
+    return s2 | (s << 8) | (s << 16) | (s3 << 24);
+}
+
+// Cooperative fill of the replicated table: T[(x << 5) | r] = T0[x].
+MH_D void aes_lds_fill(uint32_t* T, int tid, int nthreads) {
+    for (int i = tid; i < AES_LDS_WORDS; i += nthreads) T[i] = aes_t0(i >> 5);
+}
+
+struct AesLds {
+    const uint32_t* base;  // &T[lane & 31]
+    MH_D uint32_t t0(uint32_t byte_idx) const { return base[byte_idx << 5]; }
+};
+
+MH_D uint32_t rot8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+MH_D uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+MH_D uint32_t rot24(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
+
+MH_D uint32_t b0(uint32_t x) { return x & 0xffu; }
+MH_D uint32_t b1(uint32_t x) { return __builtin_amdgcn_ubfe(x, 8, 8); }
+MH_D uint32_t b2(uint32_t x) { return __builtin_amdgcn_ubfe(x, 16, 8); }
+MH_D uint32_t b3(uint32_t x) { return x >> 24; }
+
+// Encrypt one block.  rk: 44 round-key words (little-endian column words).
+MH_D void aes128_encrypt(const AesLds& T, const uint32_t* rk, uint32_t s[4]) {
+    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t t0 = xor3_u32(T.t0(b0(s0)), rot8(T.t0(b1(s1))), rot16(T.t0(b2(s2))));
+        uint32_t t1 = xor3_u32(T.t0(b0(s1)), rot8(T.t0(b1(s2))), rot16(T.t0(b2(s3))));
+        uint32_t t2 = xor3_u32(T.t0(b0(s2)), rot8(T.t0(b1(s3))), rot16(T.t0(b2(s0))));
+        uint32_t t3 = xor3_u32(T.t0(b0(s3)), rot8(T.t0(b1(s0))), rot16(T.t0(b2(s1))));
+        t0 = xor3_u32(t0, rot24(T.t0(b3(s3))), rk[4 * r + 0]);
+        t1 = xor3_u32(t1, rot24(T.t0(b3(s0))), rk[4 * r + 1]);
+        t2 = xor3_u32(t2, rot24(T.t0(b3(s1))), rk[4 * r + 2]);
+        t3 = xor3_u32(t3, rot24(T.t0(b3(s2))), rk[4 * r + 3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    // Final round: S-box byte = byte 1 of T0 entry.  v_perm_b32 assembles it.
+    auto sb = [&](uint32_t x) { return b1(T.t0(x)); };
+    uint32_t o0 = sb(b0(s0)) | (sb(b1(s1)) << 8) | (sb(b2(s2)) << 16) | (sb(b3(s3)) << 24);
+    uint32_t o1 = sb(b0(s1)) | (sb(b1(s2)) << 8) | (sb(b2(s3)) << 16) | (sb(b3(s0)) << 24);
+    uint32_t o2 = sb(b0(s2)) | (sb(b1(s3)) << 8) | (sb(b2(s0)) << 16) | (sb(b3(s1)) << 24);
+    uint32_t o3 = sb(b0(s3)) | (sb(b1(s0)) << 8) | (sb(b2(s1)) << 16) | (sb(b3(s2)) << 24);
+    s[0] = o0 ^ rk[40];
+    s[1] = o1 ^ rk[41];
+    s[2] = o2 ^ rk[42];
+    s[3] = o3 ^ rk[43];
+}
+
+// AES-128 key expansion (FIPS-197 §5.2) with the S-box from the LDS table.
+MH_D void aes128_expand(const AesLds& T, const uint32_t key[4], uint32_t rk[44]) {
+    rk[0] = key[0]; rk[1] = key[1]; rk[2] = key[2]; rk[3] = key[3];
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int i = 4; i < 44; i++) {
+        uint32_t t = rk[i - 1];
+        if ((i & 3) == 0) {
+            // RotWord then SubWord on little-endian words: bytes (t1, t2, t3, t0)
+            uint32_t r = b1(T.t0(b1(t))) | (b1(T.t0(b2(t))) << 8) | (b1(T.t0(b3(t))) << 16) |
+                         (b1(T.t0(b0(t))) << 24);
+            t = r ^ rcon;
+            rcon = aes_xtime(rcon);
+        }
+        rk[i] = rk[i - 4] ^ t;
+    }
+}
+
+// XofFixedKeyAes128.hash_block for counter `ctr` (< 2^32 here):
+//   x = seed ^ le128(ctr); sigma(x) = x_hi || (x_hi ^ x_lo); out = AES(sigma) ^ sigma
+MH_D void fixed_key_block(const AesLds& T, const uint32_t* rk, const uint32_t seed[4], uint32_t ctr,
+                          uint32_t out[4]) {
+    uint32_t x0 = seed[0] ^ ctr, x1 = seed[1], x2 = seed[2], x3 = seed[3];
+    uint32_t sg[4] = {x2, x3, x2 ^ x0, x3 ^ x1};
+    uint32_t c[4] = {sg[0], sg[1], sg[2], sg[3]};
+    aes128_encrypt(T, rk, c);
+    out[0] = c[0] ^ sg[0];
+    out[1] = c[1] ^ sg[1];
+    out[2] = c[2] ^ sg[2];
+    out[3] = c[3] ^ sg[3];
+}

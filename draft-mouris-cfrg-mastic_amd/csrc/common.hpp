@@ -1,0 +1,35 @@
+// Shared definitions for the MI355X Mastic aggregator (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#define MH_HD __host__ __device__ __forceinline__
+#define MH_D __device__ __forceinline__
+
+// Three-input XOR.  On gfx950 this is one v_bitop3_b32 (LUT 0x96); hipcc does
+// not fuse a ^ b ^ c on its own.
+MH_D uint32_t xor3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+struct u32x2 {
+    uint32_t lo, hi;
+};
+
+// 64-bit lane helpers on 32-bit halves (CDNA has no 64-bit bitwise ALU).
+MH_D u32x2 rotl64(u32x2 v, int r) {
+    // r is a compile-time constant at every call site; the branches fold away.
+    if (r == 0) return v;
+    if (r == 32) return u32x2{v.hi, v.lo};
+    if (r < 32)
+        return u32x2{__builtin_amdgcn_alignbit(v.lo, v.hi, 32 - r),
+                     __builtin_amdgcn_alignbit(v.hi, v.lo, 32 - r)};
+    return u32x2{__builtin_amdgcn_alignbit(v.hi, v.lo, 64 - r),
+                 __builtin_amdgcn_alignbit(v.lo, v.hi, 64 - r)};
+}
+
+MH_D u32x2 xor64(u32x2 a, u32x2 b) { return u32x2{a.lo ^ b.lo, a.hi ^ b.hi}; }
+MH_D u32x2 xor3_64(u32x2 a, u32x2 b, u32x2 c) {
+    return u32x2{xor3_u32(a.lo, b.lo, c.lo), xor3_u32(a.hi, b.hi, c.hi)};
+}

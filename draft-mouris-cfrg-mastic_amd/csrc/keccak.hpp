@@ -1,0 +1,176 @@
+// Keccak-p[1600, 12] and TurboSHAKE128 sponge plumbing for gfx950.
+//
+// One sponge per lane.  The 1600-bit state lives in 50 VGPRs as 25 {lo, hi}
+// pairs; 64-bit rotations are two v_alignbit_b32, chi is one v_bitop3_b32 per
+// half, theta's 5-way parities are two 3-input XORs per half.
+//
+// Every sponge in Mastic absorbs   prefix || body   where the prefix
+// (le16(len(dst)) || dst || u8(len(seed)) || seed) is identical for all
+// reports of a batch.  A one-thread setup kernel absorbs the prefix once
+// (PrefixState); lanes start from that state at byte position `f`, which is
+// uniform across the grid, and absorb word-aligned body words whose byte image
+// is shifted by f % 4 with v_alignbit_b32.  No per-lane dynamic indexing of
+// the state is ever needed: positions are uniform, loads are per-lane.
+#pragma once
+#include "common.hpp"
+
+#define KECCAK_RATE 168
+#define KECCAK_RATE_WORDS 42
+
+struct KState {
+    u32x2 a[25];
+};
+
+// rotation offsets r[x + 5y]
+#define KR(x, y) KECCAK_ROTC[(x) + 5 * (y)]
+static constexpr int KECCAK_ROTC[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                                        25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+
+MH_D u32x2 chi1(u32x2 a, u32x2 b, u32x2 c) {
+    // a ^ (~b & c)  == bitop3 LUT 0xD2 with (a,b,c) = (src0,src1,src2)
+    return u32x2{(uint32_t)__builtin_amdgcn_bitop3_b32(a.lo, b.lo, c.lo, 0xD2),
+                 (uint32_t)__builtin_amdgcn_bitop3_b32(a.hi, b.hi, c.hi, 0xD2)};
+}
+
+// Round constants are read as literal constants (the loop is fully unrolled).
+MH_D void keccak_p12(KState& s) {
+    static constexpr uint32_t RCL[12] = {0x8000808bu, 0x0000008bu, 0x00008089u, 0x00008003u,
+                                         0x00008002u, 0x00000080u, 0x0000800au, 0x8000000au,
+                                         0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+    static constexpr uint32_t RCH[12] = {0x00000000u, 0x80000000u, 0x80000000u, 0x80000000u,
+                                         0x80000000u, 0x80000000u, 0x00000000u, 0x80000000u,
+                                         0x80000000u, 0x80000000u, 0x00000000u, 0x80000000u};
+    u32x2* A = s.a;
+#pragma unroll
+    for (int round = 0; round < 12; round++) {
+        u32x2 C[5], D[5];
+#pragma unroll
+        for (int x = 0; x < 5; x++) {
+            u32x2 t = xor3_64(A[x], A[x + 5], A[x + 10]);
+            C[x] = xor3_64(t, A[x + 15], A[x + 20]);
+        }
+#pragma unroll
+        for (int x = 0; x < 5; x++) D[x] = xor64(C[(x + 4) % 5], rotl64(C[(x + 1) % 5], 1));
+        u32x2 B[25];
+#pragma unroll
+        for (int x = 0; x < 5; x++)
+#pragma unroll
+            for (int y = 0; y < 5; y++)
+                B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(xor64(A[x + 5 * y], D[x]), KR(x, y));
+#pragma unroll
+        for (int y = 0; y < 5; y++)
+#pragma unroll
+            for (int x = 0; x < 5; x++)
+                A[x + 5 * y] = chi1(B[x + 5 * y], B[(x + 1) % 5 + 5 * y], B[(x + 2) % 5 + 5 * y]);
+        A[0].lo ^= RCL[round];
+        A[0].hi ^= RCH[round];
+    }
+}
+
+MH_D uint32_t kword(const KState& s, int j) {  // j must be a compile-time constant
+    return (j & 1) ? s.a[j >> 1].hi : s.a[j >> 1].lo;
+}
+MH_D void kxor_word(KState& s, int j, uint32_t v) {  // j compile-time constant
+    if (j & 1) s.a[j >> 1].hi ^= v; else s.a[j >> 1].lo ^= v;
+}
+
+// Absorb `nbytes` body bytes given as little-endian 32-bit words ld(m),
+// m in [0, ceil(nbytes/4)), into a sponge currently filled up to byte f of its
+// block.  f is uniform.  Bytes of the last word past nbytes must be zero.
+// Returns the new fill position.
+template <class Loader>
+MH_D int sponge_absorb_words(KState& s, int f, int nbytes, Loader ld) {
+    if (nbytes <= 0) return f;
+    const int q = f >> 2;
+    const int sh = f & 3;
+    const int nw = (nbytes + 3) >> 2;
+    const int end = f + nbytes;
+    for (int b = 0;; b++) {
+        const int base = KECCAK_RATE_WORDS * b - q;
+        uint32_t prev = (base - 1 >= 0 && base - 1 < nw) ? ld(base - 1) : 0u;
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS; j++) {
+            const int m = base + j;
+            uint32_t cur = (m >= 0 && m < nw) ? ld(m) : 0u;
+            uint32_t w = sh ? __builtin_amdgcn_alignbit(cur, prev, 32 - 8 * sh) : cur;
+            prev = cur;
+            kxor_word(s, j, w);
+        }
+        if (end >= KECCAK_RATE * (b + 1)) {
+            keccak_p12(s);
+            if (end == KECCAK_RATE * (b + 1)) return 0;
+        } else {
+            return end - KECCAK_RATE * b;
+        }
+    }
+}
+
+// TurboSHAKE padding: domain byte at position f, 0x80 into byte 167, permute.
+MH_D void sponge_pad(KState& s, int f, uint32_t domain) {
+    const int q = f >> 2;
+    const uint32_t dw = domain << (8 * (f & 3));
+#pragma unroll
+    for (int j = 0; j < KECCAK_RATE_WORDS; j++)
+        if (j == q) kxor_word(s, j, dw);
+    s.a[20].hi ^= 0x80000000u;
+    keccak_p12(s);
+}
+
+// Squeeze next_vec(field, count) from a padded sponge: stream words are read in
+// order, every W32 of them form a little-endian candidate, candidates >= p
+// are skipped (vdaf_poc.xof.Xof.next_vec).  `put(e, words)` stores element e.
+// Lanes may consume different numbers of candidates (rejection), so the loop
+// runs until every lane of the wave is done.
+template <int W32, class Valid, class Put>
+MH_D void sponge_squeeze_vec(KState& s, int count, Valid valid, Put put) {
+    uint32_t cand[W32];
+#pragma unroll
+    for (int i = 0; i < W32; i++) cand[i] = 0;
+    int e = 0;
+    int t = 0;  // stream word index (uniform)
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS; j++) {
+#pragma unroll
+            for (int i = 0; i < W32 - 1; i++) cand[i] = cand[i + 1];
+            cand[W32 - 1] = kword(s, j);
+            if (((t + j) % W32) == W32 - 1) {
+                if (e < count && valid(cand)) {
+                    put(e, cand);
+                    e++;
+                }
+            }
+        }
+        t += KECCAK_RATE_WORDS;
+        if (!__any(e < count)) break;
+        keccak_p12(s);
+    }
+}
+
+// Squeeze raw bytes (derive_seed / XOF.next(n)), n a multiple of 4 <= 168.
+template <class Put>
+MH_D void sponge_squeeze_words(const KState& s, int nwords, Put put) {
+#pragma unroll
+    for (int j = 0; j < KECCAK_RATE_WORDS; j++)
+        if (j < nwords) put(j, kword(s, j));
+}
+
+// Generic byte absorb with dynamic positions, for one-thread setup kernels.
+MH_D int sponge_absorb_bytes_slow(KState& s, int f, const uint8_t* p, int n) {
+    for (int i = 0; i < n; i++) {
+        int w = f >> 2;
+        uint32_t v = (uint32_t)p[i] << (8 * (f & 3));
+        if (w & 1) s.a[w >> 1].hi ^= v; else s.a[w >> 1].lo ^= v;
+        f++;
+        if (f == KECCAK_RATE) {
+            keccak_p12(s);
+            f = 0;
+        }
+    }
+    return f;
+}
+
+MH_D void kstate_zero(KState& s) {
+#pragma unroll
+    for (int i = 0; i < 25; i++) s.a[i] = u32x2{0, 0};
+}

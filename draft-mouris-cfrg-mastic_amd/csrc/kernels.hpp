@@ -1,0 +1,640 @@
+// HIP kernels of the batched Mastic aggregator (gfx950).
+//
+// Data layout in HBM: every per-report vector is stored as word PLANES,
+// plane[w][stride] with stride = reports padded to a multiple of 64, so lane
+// r of a wave always touches word r of a plane: all loads/stores coalesce.
+// The tree shape (agg_param) is shared by every report of a batch, so all
+// control flow below is wave-uniform; only data differs per lane.
+//
+// Reference mapping (poc/):
+//   k_eval_level   Vidpf.eval_with_siblings / eval_next / extend / convert /
+//                  node_proof (vidpf.py:213-380) for one tree level, plus the
+//                  per-parent payload difference of Mastic.prep_init
+//                  (mastic.py:267-271) and the truncated out shares (:311-314)
+//   k_absorb       the one-hot / payload binders' TurboSHAKE absorption
+//                  (mastic.py:259-287), streamed level by level
+//   k_finalize     payload/onehot checks, counter check, eval proof (:277-306)
+//   k_flp_rand     query rand, helper proof share, joint rand (:437-510)
+//   k_flp_query    FlpBBCGGI19.query (:250-256)
+//   k_fold         agg_update / merge over reports (:379-397)
+//   k_decide       prep_shares_to_prep (:320-362)
+//   k_shard        client Mastic.shard (:91-185) incl. Vidpf.gen (vidpf.py:103-211)
+#pragma once
+#include "aes.hpp"
+#include "flp.hpp"
+#include "keccak.hpp"
+
+// ------------------------------------------------------------- prefix states
+enum PfxId {
+    PFX_EXT = 0,        // XofFixedKeyAes128 key, usage EXTEND  (D = 2)
+    PFX_CONV,           // XofFixedKeyAes128 key, usage CONVERT (D = 2)
+    PFX_NODE,           // node proof, seed length 16
+    PFX_ONEHOT,         // onehot check, empty seed
+    PFX_PAYLOAD,        // payload check, empty seed
+    PFX_EVAL,           // eval proof, verify key as seed
+    PFX_QUERY,          // query rand, verify key as seed
+    PFX_PROOF_SHARE,    // helper proof share, 32-byte seed follows
+    PFX_JR_PART,        // joint rand part, 32-byte seed follows
+    PFX_JR_SEED,        // joint rand seed, empty seed
+    PFX_JR,             // joint rand, 32-byte seed follows
+    PFX_PROVE_RAND,     // prove rand (client), 32-byte seed follows
+    PFX_COUNT
+};
+
+struct PrefixState {
+    KState st;
+    int f;
+    int pad[3];
+};
+
+__global__ void k_prefix_states(const uint8_t* bytes, const int* offs, const int* lens, int count,
+                                PrefixState* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int i = 0; i < count; i++) {
+        KState s;
+        kstate_zero(s);
+        int f = sponge_absorb_bytes_slow(s, 0, bytes + offs[i], lens[i]);
+        out[i].st = s;
+        out[i].f = f;
+    }
+}
+
+MH_D void load_prefix(const PrefixState* ps, int id, KState& s, int& f) {
+    s = ps[id].st;
+    f = ps[id].f;
+}
+
+MH_D uint32_t ld_u32_bytes(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// ------------------------------------------------------------- planes
+struct Planes {
+    int n, stride;
+    // report inputs (unpacked)
+    uint32_t* key;       // [4]
+    uint32_t* nonce;     // [4]
+    uint32_t* cw_seed;   // [bits][4]
+    uint32_t* cw_ctrl;   // [bits]
+    uint32_t* cw_w;      // [bits][vl*w32]
+    uint32_t* cw_proof;  // [bits][8]
+    uint32_t* lps;       // [proof_len*w32] leader proof share (agg 0)
+    uint32_t* seed;      // [8]  FLP seed (agg 1: helper seed, agg 0: leader seed)
+    uint32_t* peer;      // [8]  peer joint rand part
+    uint32_t* rk_ext;    // [44]
+    uint32_t* rk_conv;   // [44]
+    // sponges
+    uint32_t* sp_onehot;   // [50]
+    uint32_t* sp_payload;  // [50]
+    // results
+    uint32_t* rootsum;     // [vl*w32]   w_L0 + w_R0 (raw)
+    uint32_t* beta;        // [vl*w32]   beta share (negated for agg 1)
+    uint32_t* eval_proof;  // [8]
+    uint32_t* proof;       // [proof_len*w32]
+    uint32_t* qr;          // [qrl*w32]
+    uint32_t* jr;          // [jrl*w32]
+    uint32_t* jr_part;     // [8]
+    uint32_t* jr_seed;     // [8]
+    uint32_t* verifier;    // [verifier_len*w32]
+    int32_t* status;       // [1]
+};
+
+// ------------------------------------------------------------- unpack
+// Wire public share: pack_bits(ctrl) || seed_cw[B] || w_cw[B] || proof_cw[B]
+// (poc/vidpf.py:382-394).  Input share: key || [leader proof share] || [seed]
+// || [peer jr part] (poc/mastic.py:516-529).
+__global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_id, const uint8_t* nonces,
+                                                const uint8_t* pub, const uint8_t* ins) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= pl.n) return;
+    const int S = pl.stride;
+    const size_t ps_size = mc_public_share_size(p);
+    const size_t is_size = mc_input_share_size(p, agg_id);
+    const uint8_t* ps = pub + ps_size * r;
+    const uint8_t* is = ins + is_size * r;
+    const uint8_t* nc = nonces + 16 * (size_t)r;
+    const int nctrl = (2 * p.bits + 7) / 8;
+    const int wl = p.value_len * p.w32;
+    for (int i = 0; i < 4; i++) {
+        pl.nonce[i * S + r] = ld_u32_bytes(nc + 4 * i);
+        pl.key[i * S + r] = ld_u32_bytes(is + 4 * i);
+    }
+    for (int l = 0; l < p.bits; l++) {
+        uint32_t c0 = (ps[(2 * l) >> 3] >> ((2 * l) & 7)) & 1;
+        uint32_t c1 = (ps[(2 * l + 1) >> 3] >> ((2 * l + 1) & 7)) & 1;
+        pl.cw_ctrl[(size_t)l * S + r] = c0 | (c1 << 1);
+        for (int i = 0; i < 4; i++)
+            pl.cw_seed[((size_t)l * 4 + i) * S + r] = ld_u32_bytes(ps + nctrl + 16 * l + 4 * i);
+        const uint8_t* wsrc = ps + nctrl + 16 * p.bits + (size_t)l * p.value_len * p.enc;
+        for (int k = 0; k < wl; k++) pl.cw_w[((size_t)l * wl + k) * S + r] = ld_u32_bytes(wsrc + 4 * k);
+        const uint8_t* psrc = ps + nctrl + 16 * p.bits + (size_t)p.bits * p.value_len * p.enc + 32 * l;
+        for (int i = 0; i < 8; i++) pl.cw_proof[((size_t)l * 8 + i) * S + r] = ld_u32_bytes(psrc + 4 * i);
+    }
+    const uint8_t* q = is + 16;
+    if (agg_id == 0) {
+        for (int k = 0; k < p.proof_len * p.w32; k++) pl.lps[(size_t)k * S + r] = ld_u32_bytes(q + 4 * k);
+        q += (size_t)p.proof_len * p.enc;
+    }
+    if (agg_id == 1 || p.joint_rand_len > 0) {
+        for (int i = 0; i < 8; i++) pl.seed[i * S + r] = ld_u32_bytes(q + 4 * i);
+        q += 32;
+    }
+    if (p.joint_rand_len > 0)
+        for (int i = 0; i < 8; i++) pl.peer[i * S + r] = ld_u32_bytes(q + 4 * i);
+}
+
+// ------------------------------------------------------------- key setup
+// The two fixed AES keys of a report depend only on (ctx, usage, nonce)
+// (vdaf_poc XofFixedKeyAes128): derive them once, expand once.
+__global__ __launch_bounds__(256) void k_setup(Planes pl, const PrefixState* pfx) {
+    __shared__ uint32_t T[AES_LDS_WORDS];
+    aes_lds_fill(T, threadIdx.x, 256);
+    __syncthreads();
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= pl.stride) return;
+    const int S = pl.stride;
+    AesLds TL{T + (threadIdx.x & 31)};
+    for (int which = 0; which < 2; which++) {
+        KState s;
+        int f;
+        load_prefix(pfx, which == 0 ? PFX_EXT : PFX_CONV, s, f);
+        f = sponge_absorb_words(s, f, 16, [&](int m) { return pl.nonce[m * S + r]; });
+        sponge_pad(s, f, 0x02);
+        uint32_t key[4] = {s.a[0].lo, s.a[0].hi, s.a[1].lo, s.a[1].hi};
+        uint32_t rk[44];
+        aes128_expand(TL, key, rk);
+        uint32_t* dst = which == 0 ? pl.rk_ext : pl.rk_conv;
+#pragma unroll
+        for (int i = 0; i < 44; i++) dst[i * S + r] = rk[i];
+    }
+    KState s;
+    int f;
+    load_prefix(pfx, PFX_ONEHOT, s, f);
+#pragma unroll
+    for (int i = 0; i < 25; i++) {
+        pl.sp_onehot[(2 * i) * S + r] = s.a[i].lo;
+        pl.sp_onehot[(2 * i + 1) * S + r] = s.a[i].hi;
+    }
+    load_prefix(pfx, PFX_PAYLOAD, s, f);
+#pragma unroll
+    for (int i = 0; i < 25; i++) {
+        pl.sp_payload[(2 * i) * S + r] = s.a[i].lo;
+        pl.sp_payload[(2 * i + 1) * S + r] = s.a[i].hi;
+    }
+}
+
+// ------------------------------------------------------------- convert stream
+// XofFixedKeyAes128(seed, dst(ctx, CONVERT), nonce) after next(16):
+// next_vec(field, VALUE_LEN) with rejection of candidates >= p.
+template <class F> struct ConvStream;
+
+template <> struct ConvStream<F64> {
+    uint32_t seed[4];
+    uint32_t blk[4];
+    uint32_t ctr;
+    uint32_t half;
+    MH_D void init(const uint32_t s[4]) {
+        seed[0] = s[0]; seed[1] = s[1]; seed[2] = s[2]; seed[3] = s[3];
+        ctr = 1;
+        half = 2;
+    }
+    MH_D uint64_t next(const AesLds& T, const uint32_t* rk) {
+        uint64_t v;
+        do {
+            if (half == 2) {
+                fixed_key_block(T, rk, seed, ctr, blk);
+                ctr++;
+                half = 0;
+            }
+            v = half ? (((uint64_t)blk[3] << 32) | blk[2]) : (((uint64_t)blk[1] << 32) | blk[0]);
+            half++;
+        } while (!F64::valid(v));
+        return v;
+    }
+};
+
+template <> struct ConvStream<F128> {
+    uint32_t seed[4];
+    uint32_t ctr;
+    MH_D void init(const uint32_t s[4]) {
+        seed[0] = s[0]; seed[1] = s[1]; seed[2] = s[2]; seed[3] = s[3];
+        ctr = 1;
+    }
+    MH_D F128::E next(const AesLds& T, const uint32_t* rk) {
+        F128::E v;
+        do {
+            uint32_t b[4];
+            fixed_key_block(T, rk, seed, ctr, b);
+            ctr++;
+            v = F128::from_words(b);
+        } while (!F128::valid(v));
+        return v;
+    }
+};
+
+// ------------------------------------------------------------- eval level
+struct LevelArgs {
+    int level;
+    int last_level;      // L (agg param level)
+    int agg_id;
+    int n_parents;       // parents evaluated at this level (1 = the root at level 0)
+    int ppw;             // parents per wave
+    int path_bytes;      // ceil((level + 1) / 8)
+    int n_prefixes;
+    const int32_t* child_exp;    // [2 * n_parents] index into this level's frontier, -1 = leaf
+    const int32_t* child_pfx;    // [2 * n_parents] index into the prefix list (level L), -1 = none
+    const uint32_t* child_path;  // [2 * n_parents][8] MSB-first packed path words
+    // frontier planes (seed [e][4], ctrl [e], w [e][vl*w32])
+    const uint32_t* fr_seed_in;
+    const uint32_t* fr_ctrl_in;
+    const uint32_t* fr_w_in;
+    uint32_t* fr_seed_out;
+    uint32_t* fr_ctrl_out;
+    uint32_t* fr_w_out;
+    uint32_t* onehot;    // [2 * n_parents * 8]   node proofs of this level (BFS order)
+    uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents
+    uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
+};
+
+template <class F>
+__global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, LevelArgs a, const PrefixState* pfx) {
+    typedef typename F::E E;
+    __shared__ uint32_t T[AES_LDS_WORDS];
+    __shared__ uint32_t V[16 * 256];  // node-proof message staging, [word][thread]
+    aes_lds_fill(T, threadIdx.x, 256);
+    __syncthreads();
+
+    const int S = pl.stride;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = blockIdx.x * 64 + lane;
+    const int pbeg = (blockIdx.y * 4 + wave) * a.ppw;
+    if (pbeg >= a.n_parents) return;
+    const int pend = min(pbeg + a.ppw, a.n_parents);
+    const int l = a.level;
+    const int vl = p.value_len;
+    const int wl = vl * F::W32;
+    AesLds TL{T + (lane & 31)};
+
+    uint32_t rke[44], rkc[44];
+#pragma unroll
+    for (int i = 0; i < 44; i++) {
+        rke[i] = pl.rk_ext[i * S + r];
+        rkc[i] = pl.rk_conv[i * S + r];
+    }
+    uint32_t scw[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) scw[i] = pl.cw_seed[((size_t)l * 4 + i) * S + r];
+    const uint32_t ccw = pl.cw_ctrl[(size_t)l * S + r];
+    const uint32_t* wcw = pl.cw_w + (size_t)l * wl * S;
+
+    KState s0;
+    int f0;
+    load_prefix(pfx, PFX_NODE, s0, f0);
+
+    for (int pi = pbeg; pi < pend; pi++) {
+        // parent seed / control bit
+        uint32_t ps[4];
+        uint32_t pctrl;
+        if (l == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) ps[i] = pl.key[i * S + r];
+            pctrl = a.agg_id;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) ps[i] = a.fr_seed_in[((size_t)pi * 4 + i) * S + r];
+            pctrl = a.fr_ctrl_in[(size_t)pi * S + r];
+        }
+        // extend (block c belongs to child c) + correct, then the convert seed block
+        uint32_t cs[2][4], ns[2][4], tc[2];
+#pragma unroll 1
+        for (int c = 0; c < 2; c++) {
+            uint32_t b[4];
+            fixed_key_block(TL, rke, ps, (uint32_t)c, b);
+            uint32_t t = b[0] & 1u;
+            b[0] &= ~1u;
+            if (pctrl) {
+                b[0] ^= scw[0]; b[1] ^= scw[1]; b[2] ^= scw[2]; b[3] ^= scw[3];
+                t ^= (ccw >> c) & 1u;
+            }
+            uint32_t nb[4];
+            fixed_key_block(TL, rkc, b, 0u, nb);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                cs[c][i] = b[i];
+                ns[c][i] = nb[i];
+            }
+            tc[c] = t;
+        }
+        const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
+        const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
+
+        // payloads of both children, element by element
+        ConvStream<F> st0, st1;
+        st0.init(cs[0]);
+        st1.init(cs[1]);
+        E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
+        const int row = 1 + p.output_len;
+        for (int e = 0; e < vl; e++) {
+            E x0 = st0.next(TL, rkc);
+            E x1 = st1.next(TL, rkc);
+            E cw = pl_load<F>(wcw, e, S, r);
+            if (tc[0]) x0 = F::add(x0, cw);
+            if (tc[1]) x1 = F::add(x1, cw);
+            if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
+            if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
+            if (l == 0) {
+                pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
+            } else {
+                E wp = pl_load<F>(a.fr_w_in, pi * vl + e, S, r);
+                pl_store<F>(a.payload, pi * vl + e, S, r, F::sub(F::sub(wp, x0), x1));
+            }
+            if (pf0 >= 0 || pf1 >= 0) {
+                // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
+                if (e == 0) {
+                    if (pf0 >= 0) pl_store<F>(a.out, pf0 * row, S, r, a.agg_id ? F::neg(x0) : x0);
+                    if (pf1 >= 0) pl_store<F>(a.out, pf1 * row, S, r, a.agg_id ? F::neg(x1) : x1);
+                } else if (e - 1 < p.tlimit) {
+                    const int m = e - 1;
+                    const int g = m % p.tgroup;
+                    if (p.tgroup == 1) {
+                        acc0 = x0;
+                        acc1 = x1;
+                    } else {
+                        coef = g == 0 ? F::from_u64(1) : F::add(coef, coef);
+                        acc0 = F::add(g == 0 ? F::zero() : acc0, F::mul(coef, x0));
+                        acc1 = F::add(g == 0 ? F::zero() : acc1, F::mul(coef, x1));
+                    }
+                    if (g == p.tgroup - 1) {
+                        const int o = 1 + m / p.tgroup;
+                        if (pf0 >= 0) pl_store<F>(a.out, pf0 * row + o, S, r, a.agg_id ? F::neg(acc0) : acc0);
+                        if (pf1 >= 0) pl_store<F>(a.out, pf1 * row + o, S, r, a.agg_id ? F::neg(acc1) : acc1);
+                    }
+                }
+            }
+        }
+
+        // node proofs: TurboSHAKE128(seed, dst(ctx, NODE_PROOF), le16(BITS) || le16(l) || path)
+#pragma unroll 1
+        for (int c = 0; c < 2; c++) {
+            const int node = 2 * pi + c;
+            V[0 * 256 + threadIdx.x] = ns[c][0];
+            V[1 * 256 + threadIdx.x] = ns[c][1];
+            V[2 * 256 + threadIdx.x] = ns[c][2];
+            V[3 * 256 + threadIdx.x] = ns[c][3];
+            V[4 * 256 + threadIdx.x] = (uint32_t)p.bits | ((uint32_t)l << 16);
+            const int pw = (a.path_bytes + 3) >> 2;
+            for (int i = 0; i < pw; i++) V[(5 + i) * 256 + threadIdx.x] = a.child_path[node * 8 + i];
+            KState s = s0;
+            int f = sponge_absorb_words(s, f0, 20 + a.path_bytes,
+                                        [&](int m) { return V[m * 256 + threadIdx.x]; });
+            sponge_pad(s, f, 0x01);
+            const bool t = tc[c] != 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                uint32_t w = kword(s, j);
+                if (t) w ^= pl.cw_proof[((size_t)l * 8 + j) * S + r];
+                a.onehot[((size_t)node * 8 + j) * S + r] = w;
+            }
+            const int ce = c ? ce1 : ce0;
+            if (ce >= 0) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) a.fr_seed_out[((size_t)ce * 4 + i) * S + r] = ns[c][i];
+                a.fr_ctrl_out[(size_t)ce * S + r] = tc[c];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- binder absorb
+// Continues the one-hot (sponge 0) or payload (sponge 1) TurboSHAKE over the
+// words one level produced.  Positions are uniform (tracked by the host).
+struct AbsorbArgs {
+    const uint32_t* seg[2];
+    int nbytes[2];
+    int f[2];
+};
+
+__global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    const int which = blockIdx.y;
+    if (r >= pl.stride) return;
+    const int nb = a.nbytes[which];
+    if (nb == 0) return;
+    const int S = pl.stride;
+    uint32_t* sp = which == 0 ? pl.sp_onehot : pl.sp_payload;
+    const uint32_t* seg = a.seg[which];
+    KState s;
+#pragma unroll
+    for (int i = 0; i < 25; i++) s.a[i] = u32x2{sp[(2 * i) * S + r], sp[(2 * i + 1) * S + r]};
+    sponge_absorb_words(s, a.f[which], nb, [&](int m) { return seg[(size_t)m * S + r]; });
+#pragma unroll
+    for (int i = 0; i < 25; i++) {
+        sp[(2 * i) * S + r] = s.a[i].lo;
+        sp[(2 * i + 1) * S + r] = s.a[i].hi;
+    }
+}
+
+// ------------------------------------------------------------- finalize
+// payload_check, onehot_check, counter_check, eval_proof (mastic.py:277-306).
+struct FinalArgs {
+    int agg_id;
+    int f_onehot;
+    int f_payload;
+};
+
+template <class F>
+__global__ __launch_bounds__(256) void k_finalize(McParams p, Planes pl, FinalArgs a, const PrefixState* pfx) {
+    __shared__ uint32_t V[24 * 256];
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= pl.stride) return;
+    const int S = pl.stride;
+    uint32_t oh[8], pc[8];
+    {
+        KState s;
+#pragma unroll
+        for (int i = 0; i < 25; i++) s.a[i] = u32x2{pl.sp_onehot[(2 * i) * S + r], pl.sp_onehot[(2 * i + 1) * S + r]};
+        sponge_pad(s, a.f_onehot, 0x01);
+#pragma unroll
+        for (int j = 0; j < 8; j++) oh[j] = kword(s, j);
+#pragma unroll
+        for (int i = 0; i < 25; i++) s.a[i] = u32x2{pl.sp_payload[(2 * i) * S + r], pl.sp_payload[(2 * i + 1) * S + r]};
+        sponge_pad(s, a.f_payload, 0x01);
+#pragma unroll
+        for (int j = 0; j < 8; j++) pc[j] = kword(s, j);
+    }
+    typename F::E cnt = F::add(pl_load<F>(pl.rootsum, 0, S, r), F::from_u64((uint64_t)a.agg_id));
+    // body = onehot_check || counter_check || payload_check
+    const int t = threadIdx.x;
+    for (int j = 0; j < 8; j++) V[j * 256 + t] = oh[j];
+    for (int j = 0; j < F::W32; j++) V[(8 + j) * 256 + t] = F::word(cnt, j);
+    for (int j = 0; j < 8; j++) V[(8 + F::W32 + j) * 256 + t] = pc[j];
+    KState s;
+    int f;
+    load_prefix(pfx, PFX_EVAL, s, f);
+    f = sponge_absorb_words(s, f, 64 + F::ENC, [&](int m) { return V[m * 256 + t]; });
+    sponge_pad(s, f, 0x01);
+#pragma unroll
+    for (int j = 0; j < 8; j++) pl.eval_proof[j * S + r] = kword(s, j);
+}
+
+// ------------------------------------------------------------- FLP randomness
+template <class F, class Put>
+MH_D void squeeze_elems(KState& s, int count, Put put) {
+    sponge_squeeze_vec<F::W32>(
+        s, count, [&](const uint32_t* w) { return F::valid(F::from_words(w)); },
+        [&](int e, const uint32_t* w) { put(e, F::from_words(w)); });
+}
+
+struct FlpArgs {
+    int agg_id;
+    int level;
+};
+
+template <class F>
+__global__ __launch_bounds__(256) void k_flp_rand(McParams p, Planes pl, FlpArgs a, const PrefixState* pfx) {
+    typedef typename F::E E;
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= pl.stride) return;
+    const int S = pl.stride;
+    // beta share (get_beta_share, vidpf.py:263-279): w_L0 + w_R0, negated by the helper
+    for (int e = 0; e < p.value_len; e++) {
+        E x = pl_load<F>(pl.rootsum, e, S, r);
+        pl_store<F>(pl.beta, e, S, r, a.agg_id ? F::neg(x) : x);
+    }
+    KState s;
+    int f;
+    // query rand: TS(verify_key, dst_alg(ctx, QUERY_RAND), nonce || le16(level))
+    load_prefix(pfx, PFX_QUERY, s, f);
+    f = sponge_absorb_words(s, f, 18, [&](int m) {
+        return m < 4 ? pl.nonce[m * S + r] : (uint32_t)(a.level & 0xffff);
+    });
+    sponge_pad(s, f, 0x01);
+    squeeze_elems<F>(s, p.query_rand_len, [&](int e, E x) { pl_store<F>(pl.qr, e, S, r, x); });
+    // proof share: leader from the input share, helper expands its seed
+    if (a.agg_id == 0) {
+        for (int k = 0; k < p.proof_len * F::W32; k++) pl.proof[(size_t)k * S + r] = pl.lps[(size_t)k * S + r];
+    } else {
+        load_prefix(pfx, PFX_PROOF_SHARE, s, f);
+        f = sponge_absorb_words(s, f, 32, [&](int m) { return pl.seed[m * S + r]; });
+        sponge_pad(s, f, 0x01);
+        squeeze_elems<F>(s, p.proof_len, [&](int e, E x) { pl_store<F>(pl.proof, e, S, r, x); });
+    }
+    if (p.joint_rand_len > 0) {
+        // part = TS(seed, dst_alg(JOINT_RAND_PART), nonce || encode(beta_share[1:]))
+        load_prefix(pfx, PFX_JR_PART, s, f);
+        const int mw = p.meas_len * F::W32;
+        f = sponge_absorb_words(s, f, 32 + 16 + mw * 4, [&](int m) {
+            if (m < 8) return pl.seed[m * S + r];
+            if (m < 12) return pl.nonce[(m - 8) * S + r];
+            return pl.beta[(size_t)(F::W32 + m - 12) * S + r];
+        });
+        sponge_pad(s, f, 0x01);
+        uint32_t part[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            part[j] = kword(s, j);
+            pl.jr_part[j * S + r] = part[j];
+        }
+        // seed = TS(b'', dst_alg(JOINT_RAND_SEED), part_0 || part_1)
+        load_prefix(pfx, PFX_JR_SEED, s, f);
+        const bool leader = a.agg_id == 0;
+        f = sponge_absorb_words(s, f, 64, [&](int m) {
+            const bool own = leader ? (m < 8) : (m >= 8);
+            const int j = m & 7;
+            return own ? pl.jr_part[j * S + r] : pl.peer[j * S + r];
+        });
+        sponge_pad(s, f, 0x01);
+#pragma unroll
+        for (int j = 0; j < 8; j++) pl.jr_seed[j * S + r] = kword(s, j);
+        // joint rand = TS(seed, dst_alg(JOINT_RAND), b'').next_vec(JRL)
+        load_prefix(pfx, PFX_JR, s, f);
+        f = sponge_absorb_words(s, f, 32, [&](int m) { return pl.jr_seed[m * S + r]; });
+        sponge_pad(s, f, 0x01);
+        squeeze_elems<F>(s, p.joint_rand_len, [&](int e, E x) { pl_store<F>(pl.jr, e, S, r, x); });
+    }
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_flp_query(McParams p, Planes pl, FlpConsts<F> c) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= pl.stride) return;
+    const int S = pl.stride;
+    const bool ok = flp_query<F>(p, c, pl.beta + (size_t)F::W32 * S, pl.proof, pl.qr, pl.jr, pl.verifier, S, r);
+    if (!ok) pl.status[r] = -2;  // test point is a root of unity
+}
+
+// ------------------------------------------------------------- fold
+// agg_share[i] = sum over valid reports of out[i]  (agg_update + merge).
+template <class F>
+__global__ __launch_bounds__(256) void k_fold(const uint32_t* out, int n, int stride, const uint8_t* valid,
+                                              uint32_t* agg_words) {
+    typedef typename F::E E;
+    __shared__ E red[256];
+    const int row = blockIdx.x;
+    E acc = F::zero();
+    for (int r = threadIdx.x; r < n; r += 256) {
+        if (valid && !valid[r]) continue;
+        acc = F::add(acc, pl_load<F>(out, row, stride, r));
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        E x = red[0];
+        for (int i = 0; i < F::W32; i++) agg_words[(size_t)row * F::W32 + i] = F::word(x, i);
+    }
+}
+
+// ------------------------------------------------------------- decide
+// prep_shares_to_prep (mastic.py:320-362) for a batch of report pairs.
+// prep share wire: eval_proof || [jr_part] || [verifier]  (mastic.py:543-552)
+template <class F>
+__global__ __launch_bounds__(256) void k_decide(McParams p, int n, int stride, int weight_check,
+                                                const uint8_t* ps0, const uint8_t* ps1, int ps_size,
+                                                uint32_t* ver_scratch, const PrefixState* pfx,
+                                                uint8_t* msg_out, uint8_t* status_out) {
+    typedef typename F::E E;
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t* a = ps0 + (size_t)ps_size * r;
+    const uint8_t* b = ps1 + (size_t)ps_size * r;
+    // status: 1 = valid, 0 = VIDPF verification failed, 2 = FLP verification failed
+    uint8_t st = 1;
+    for (int i = 0; i < 32; i++)
+        if (a[i] != b[i]) st = 0;
+    if (st && weight_check) {
+        const int jr = p.joint_rand_len > 0 ? 32 : 0;
+        const uint8_t* va = a + 32 + jr;
+        const uint8_t* vb = b + 32 + jr;
+        for (int e = 0; e < p.verifier_len; e++) {
+            uint32_t wa[F::W32], wb[F::W32];
+            for (int i = 0; i < F::W32; i++) {
+                wa[i] = ld_u32_bytes(va + e * F::ENC + 4 * i);
+                wb[i] = ld_u32_bytes(vb + e * F::ENC + 4 * i);
+            }
+            E xa = F::from_words(wa), xb = F::from_words(wb);
+            if (!F::valid(xa) || !F::valid(xb)) st = 2;
+            pl_store<F>(ver_scratch, e, stride, r, F::add(xa, xb));
+        }
+        if (st == 1 && !flp_decide<F>(p, ver_scratch, stride, r)) st = 2;
+        if (st == 1 && p.joint_rand_len > 0) {
+            KState s;
+            int f;
+            load_prefix(pfx, PFX_JR_SEED, s, f);
+            f = sponge_absorb_words(s, f, 64, [&](int m) {
+                return m < 8 ? ld_u32_bytes(a + 32 + 4 * m) : ld_u32_bytes(b + 32 + 4 * (m - 8));
+            });
+            sponge_pad(s, f, 0x01);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                uint32_t w = kword(s, j);
+                for (int i = 0; i < 4; i++) msg_out[(size_t)32 * r + 4 * j + i] = (uint8_t)(w >> (8 * i));
+            }
+        }
+    }
+    status_out[r] = st;
+}

@@ -1,0 +1,995 @@
+// Host side of the MI355X Mastic aggregator: C ABI (include/mastic_hip.h),
+// agg-param decoding and tree building, HBM buffer management and the
+// level-by-level launch schedule.  No CPU compute path exists: every
+// cryptographic operation of prep_init / shard / decide / aggregate runs in
+// the kernels of kernels.hpp / shard.hpp.
+#include "mastic_hip.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "shard.hpp"
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    bool ensure(size_t want) {
+        if (want <= bytes && p) return true;
+        release();
+        if (want == 0) want = 16;
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return false;
+        }
+        bytes = want;
+        return true;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+struct Tree {
+    int L = 0;
+    int n_prefixes = 0;
+    bool weight_check = false;
+    std::vector<int> n_parents;        // per level
+    std::vector<int> n_exp;            // expanded nodes per level
+    std::vector<size_t> off;           // per-level offset into the node arrays
+    std::vector<int32_t> child_exp, child_pfx;
+    std::vector<uint32_t> child_path;  // 8 words per node
+    DevBuf d_exp, d_pfx, d_path;
+    uint64_t nodes = 0, interior = 0;
+    int max_level_nodes = 0, max_exp = 0, max_parents = 0;
+};
+
+struct Result {
+    bool ready = false;
+    size_t n = 0, stride = 0;
+    int weight_check = 0;
+    int n_prefixes = 0;
+    DevBuf out, eval_proof, verifier, jr_part, jr_seed, status;
+};
+
+inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct mastic_reports {
+    mastic_ctx* ctx = nullptr;
+    size_t n = 0;
+    DevBuf nonces, pub, in0, in1;
+};
+
+struct mastic_ctx {
+    mastic_params user{};
+    McParams p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    uint64_t budget = 0;
+    DevBuf work;     // per-chunk planes
+    DevBuf pfx;      // PrefixState[PFX_COUNT]
+    DevBuf pfx_bytes, pfx_meta;
+    DevBuf consts;   // alpha^-i table for prove
+    int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
+    std::map<std::vector<uint8_t>, Tree*> trees;
+    Result res[2];
+    // timing
+    std::vector<hipEvent_t> ev;
+    double t_eval = 0, t_absorb = 0, t_total = 0;
+    int n_eval = 0, n_absorb = 0;
+    ~mastic_ctx() {
+        for (auto& kv : trees) delete kv.second;
+        for (auto e : ev) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+static int fail(mastic_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                  \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess) return fail((c), MASTIC_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+// ---------------------------------------------------------------- helpers
+static void put_le16(std::vector<uint8_t>& v, uint32_t x) {
+    v.push_back((uint8_t)x);
+    v.push_back((uint8_t)(x >> 8));
+}
+
+// dst (poc/dst.py:30-32) and dst_alg (:35-42)
+static std::vector<uint8_t> dst(const uint8_t* ctx, size_t n, int usage) {
+    std::vector<uint8_t> d = {'m', 'a', 's', 't', 'i', 'c', 0, (uint8_t)usage};
+    d.insert(d.end(), ctx, ctx + n);
+    return d;
+}
+static std::vector<uint8_t> dst_alg(const uint8_t* ctx, size_t n, int usage, uint32_t id) {
+    std::vector<uint8_t> d = {'m', 'a', 's', 't', 'i', 'c', 0, (uint8_t)usage,
+                              (uint8_t)(id >> 24), (uint8_t)(id >> 16), (uint8_t)(id >> 8), (uint8_t)id};
+    d.insert(d.end(), ctx, ctx + n);
+    return d;
+}
+
+// Compute the 12 sponge prefix states for (ctx, verify_key) on the device.
+static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* vk) {
+    static const uint8_t zero_vk[32] = {0};
+    if (!vk) vk = zero_vk;
+    if (ctx_len > 65535 - 12) return fail(c, MASTIC_EINVAL, "ctx too long");
+    std::vector<std::vector<uint8_t>> m(PFX_COUNT);
+    auto xof_ts = [&](int id, const std::vector<uint8_t>& d, int seed_len, const uint8_t* seed) {
+        put_le16(m[id], (uint32_t)d.size());
+        m[id].insert(m[id].end(), d.begin(), d.end());
+        m[id].push_back((uint8_t)seed_len);
+        if (seed) m[id].insert(m[id].end(), seed, seed + seed_len);
+    };
+    auto xof_aes = [&](int id, const std::vector<uint8_t>& d) {
+        put_le16(m[id], (uint32_t)d.size());
+        m[id].insert(m[id].end(), d.begin(), d.end());
+    };
+    const uint32_t ID = c->p.alg_id;
+    xof_aes(PFX_EXT, dst(app_ctx, ctx_len, 10));
+    xof_aes(PFX_CONV, dst(app_ctx, ctx_len, 11));
+    xof_ts(PFX_NODE, dst(app_ctx, ctx_len, 9), 16, nullptr);
+    xof_ts(PFX_ONEHOT, dst_alg(app_ctx, ctx_len, 6, ID), 0, nullptr);
+    xof_ts(PFX_PAYLOAD, dst_alg(app_ctx, ctx_len, 7, ID), 0, nullptr);
+    xof_ts(PFX_EVAL, dst_alg(app_ctx, ctx_len, 8, ID), 32, vk);
+    xof_ts(PFX_QUERY, dst_alg(app_ctx, ctx_len, 2, ID), 32, vk);
+    xof_ts(PFX_PROOF_SHARE, dst_alg(app_ctx, ctx_len, 1, ID), 32, nullptr);
+    xof_ts(PFX_JR_PART, dst_alg(app_ctx, ctx_len, 4, ID), 32, nullptr);
+    xof_ts(PFX_JR_SEED, dst_alg(app_ctx, ctx_len, 3, ID), 0, nullptr);
+    xof_ts(PFX_JR, dst_alg(app_ctx, ctx_len, 5, ID), 32, nullptr);
+    xof_ts(PFX_PROVE_RAND, dst_alg(app_ctx, ctx_len, 0, ID), 32, nullptr);
+    std::vector<uint8_t> all;
+    std::vector<int> meta(2 * PFX_COUNT);
+    for (int i = 0; i < PFX_COUNT; i++) {
+        c->pfx_f[i] = (int)(m[i].size() % KECCAK_RATE);
+        meta[i] = (int)all.size();
+        meta[PFX_COUNT + i] = (int)m[i].size();
+        all.insert(all.end(), m[i].begin(), m[i].end());
+    }
+    if (!c->pfx.ensure(sizeof(PrefixState) * PFX_COUNT) || !c->pfx_bytes.ensure(all.size()) ||
+        !c->pfx_meta.ensure(meta.size() * sizeof(int)))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (prefix states)");
+    HIPCHK(c, hipMemcpyAsync(c->pfx_bytes.p, all.data(), all.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->pfx_meta.p, meta.data(), meta.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_prefix_states, dim3(1), dim3(64), 0, c->stream, c->pfx_bytes.as<uint8_t>(),
+                       c->pfx_meta.as<int>(), c->pfx_meta.as<int>() + PFX_COUNT, (int)PFX_COUNT,
+                       c->pfx.as<PrefixState>());
+    HIPCHK(c, hipGetLastError());
+    // pfx_bytes must outlive the async kernel: keep it until the next call.
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+template <class F>
+static FlpConsts<F> flp_consts(const McParams& p) {
+    typedef typename F::E E;
+    FlpConsts<F> fc;
+    // gen = 7^GEN_BASE_EXP; alpha = gen^(GEN_ORDER / P)
+    const uint64_t gen_exp = p.field == 64 ? 4294967295ull : 4611686018427387897ull;
+    E g = fpow_u64<F>(F::from_u64(7), gen_exp);
+    int log_order = FieldConsts<F>::GEN_ORDER_LOG2;
+    int logp = 0;
+    while ((1 << logp) < p.P) logp++;
+    int sh = log_order - logp;  // exponent 2^sh
+    uint64_t ex[2] = {0, 0};
+    ex[sh / 64] = 1ull << (sh % 64);
+    fc.alpha = fpow<F>(g, ex, 2);
+    fc.inv_p = finv<F>(F::from_u64((uint64_t)p.P));
+    fc.inv2 = finv<F>(F::from_u64(2));
+    fc.offset = F::from_u64(p.offset);
+    fc.offset_h = F::mul(fc.offset, fc.inv2);
+    return fc;
+}
+
+// ---------------------------------------------------------------- tree
+// Decode Mastic.encode_agg_param (mastic.py:413-435) and build the evaluated
+// prefix tree of eval_with_siblings (vidpf.py:213-261): the children of every
+// node on a candidate-prefix path, level by level in BFS (= lexicographic)
+// order, which is the binder order of prep_init (mastic.py:263-275).
+static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out) {
+    std::vector<uint8_t> keyv(enc, enc + len);
+    auto it = c->trees.find(keyv);
+    if (it != c->trees.end()) {
+        *out = it->second;
+        return 0;
+    }
+    if (len < 7) return fail(c, MASTIC_EINVAL, "agg param too short");
+    const int level = (enc[0] << 8) | enc[1];
+    const uint64_t count = ((uint64_t)enc[2] << 24) | ((uint64_t)enc[3] << 16) | ((uint64_t)enc[4] << 8) | enc[5];
+    const size_t plen = (size_t)(level + 1 + 7) / 8;
+    if (len != 6 + plen * count + 1) return fail(c, MASTIC_EINVAL, "agg param has incorrect length");
+    if (level >= c->p.bits) return fail(c, MASTIC_EINVAL, "level too deep");
+    if (enc[len - 1] > 1) return fail(c, MASTIC_EINVAL, "invalid weight check flag");
+    const uint8_t* pre = enc + 6;
+    // prefixes as MSB-first byte strings of plen bytes (bits past level+1 must be zero)
+    const int tail_bits = (level + 1) % 8;
+    std::vector<std::vector<uint8_t>> pfx(count);
+    for (uint64_t i = 0; i < count; i++) {
+        pfx[i].assign(pre + plen * i, pre + plen * (i + 1));
+        if (tail_bits && (pfx[i][plen - 1] & ((1u << (8 - tail_bits)) - 1)))
+            return fail(c, MASTIC_EINVAL, "prefix with incorrect length");
+    }
+    {
+        std::vector<std::vector<uint8_t>> s = pfx;
+        std::sort(s.begin(), s.end());
+        if (std::adjacent_find(s.begin(), s.end()) != s.end())
+            return fail(c, MASTIC_EINVAL, "candidate prefixes are non-unique");
+    }
+    std::map<std::vector<uint8_t>, int> pfx_index;
+    for (uint64_t i = 0; i < count; i++) pfx_index[pfx[i]] = (int)i;
+
+    Tree* t = new Tree();
+    t->L = level;
+    t->n_prefixes = (int)count;
+    t->weight_check = enc[len - 1] == 1;
+    // expanded (on-path) nodes per level: distinct length-(l+1) prefixes, sorted
+    auto truncate = [](const std::vector<uint8_t>& v, int nbits) {
+        std::vector<uint8_t> r((nbits + 7) / 8);
+        for (size_t i = 0; i < r.size(); i++) r[i] = v[i];
+        if (nbits % 8) r.back() &= (uint8_t)(0xFF00u >> (nbits % 8));
+        return r;
+    };
+    std::vector<std::vector<std::vector<uint8_t>>> exp(level + 1);
+    for (int l = 0; l < level; l++) {
+        std::vector<std::vector<uint8_t>> v;
+        v.reserve(count);
+        for (auto& q : pfx) v.push_back(truncate(q, l + 1));
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        exp[l] = std::move(v);
+    }
+    std::vector<uint8_t> root;
+    size_t total = 0;
+    for (int l = 0; l <= level; l++) {
+        const std::vector<std::vector<uint8_t>>& parents =
+            l == 0 ? std::vector<std::vector<uint8_t>>{root} : exp[l - 1];
+        const int np = (int)parents.size();
+        t->n_parents.push_back(np);
+        t->n_exp.push_back(l < level ? (int)exp[l].size() : 0);
+        t->off.push_back(total);
+        for (int pi = 0; pi < np; pi++) {
+            for (int cbit = 0; cbit < 2; cbit++) {
+                std::vector<uint8_t> path = parents[pi];
+                path.resize((l + 1 + 7) / 8, 0);
+                if (cbit) path[l / 8] |= (uint8_t)(0x80u >> (l % 8));
+                int ce = -1, cp = -1;
+                if (l < level) {
+                    auto f = std::lower_bound(exp[l].begin(), exp[l].end(), path);
+                    if (f != exp[l].end() && *f == path) ce = (int)(f - exp[l].begin());
+                } else {
+                    auto f = pfx_index.find(path);
+                    if (f != pfx_index.end()) cp = f->second;
+                }
+                t->child_exp.push_back(ce);
+                t->child_pfx.push_back(cp);
+                uint32_t w[8] = {0};
+                for (size_t b = 0; b < path.size(); b++) w[b / 4] |= (uint32_t)path[b] << (8 * (b % 4));
+                for (int k = 0; k < 8; k++) t->child_path.push_back(w[k]);
+            }
+        }
+        total += 2 * (size_t)np;
+        t->max_level_nodes = std::max(t->max_level_nodes, 2 * np);
+        t->max_parents = std::max(t->max_parents, np);
+        t->max_exp = std::max(t->max_exp, t->n_exp.back());
+        if (l > 0) t->interior += np;
+    }
+    t->nodes = total;
+    if (!t->d_exp.ensure(total * 4) || !t->d_pfx.ensure(total * 4) || !t->d_path.ensure(total * 32)) {
+        delete t;
+        return fail(c, MASTIC_ENOMEM, "out of device memory (tree)");
+    }
+    hipError_t e1 = hipMemcpy(t->d_exp.p, t->child_exp.data(), total * 4, hipMemcpyHostToDevice);
+    hipError_t e2 = hipMemcpy(t->d_pfx.p, t->child_pfx.data(), total * 4, hipMemcpyHostToDevice);
+    hipError_t e3 = hipMemcpy(t->d_path.p, t->child_path.data(), total * 32, hipMemcpyHostToDevice);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        delete t;
+        return fail(c, MASTIC_EHIP, "tree upload failed");
+    }
+    if (c->trees.size() > 64) {
+        for (auto& kv : c->trees) delete kv.second;
+        c->trees.clear();
+    }
+    c->trees[keyv] = t;
+    *out = t;
+    return 0;
+}
+
+// ---------------------------------------------------------------- work layout
+struct WorkLayout {
+    size_t words = 0;  // per report (plane count)
+    size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
+        rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, fr_seed[2], fr_ctrl[2],
+        fr_w[2], onehot, payload, out;
+};
+
+static WorkLayout work_layout(const McParams& p, const Tree* t) {
+    WorkLayout w;
+    size_t o = 0;
+    auto take = [&](size_t n) {
+        size_t r = o;
+        o += n;
+        return r;
+    };
+    const size_t wl = (size_t)p.value_len * p.w32;
+    w.key = take(4);
+    w.nonce = take(4);
+    w.cw_seed = take((size_t)p.bits * 4);
+    w.cw_ctrl = take(p.bits);
+    w.cw_w = take((size_t)p.bits * wl);
+    w.cw_proof = take((size_t)p.bits * 8);
+    w.lps = take((size_t)p.proof_len * p.w32);
+    w.seed = take(8);
+    w.peer = take(8);
+    w.rk_ext = take(44);
+    w.rk_conv = take(44);
+    w.sp_onehot = take(50);
+    w.sp_payload = take(50);
+    w.rootsum = take(wl);
+    w.beta = take(wl);
+    w.eval_proof = take(8);
+    w.proof = take((size_t)p.proof_len * p.w32);
+    w.qr = take((size_t)p.query_rand_len * p.w32);
+    w.jr = take((size_t)std::max(p.joint_rand_len, 1) * p.w32);
+    w.jr_part = take(8);
+    w.jr_seed = take(8);
+    w.verifier = take((size_t)p.verifier_len * p.w32);
+    w.status = take(1);
+    for (int s = 0; s < 2; s++) {
+        w.fr_seed[s] = take((size_t)std::max(t->max_exp, 1) * 4);
+        w.fr_ctrl[s] = take(std::max(t->max_exp, 1));
+        w.fr_w[s] = take((size_t)std::max(t->max_exp, 1) * wl);
+    }
+    w.onehot = take((size_t)t->max_level_nodes * 8);
+    w.payload = take((size_t)t->max_parents * wl);
+    w.out = take((size_t)std::max(t->n_prefixes, 1) * (1 + p.output_len) * p.w32);
+    w.words = o;
+    return w;
+}
+
+static Planes make_planes(uint32_t* base, const WorkLayout& w, int n, int stride) {
+    Planes pl;
+    pl.n = n;
+    pl.stride = stride;
+    auto P = [&](size_t off) { return base + off * stride; };
+    pl.key = P(w.key);
+    pl.nonce = P(w.nonce);
+    pl.cw_seed = P(w.cw_seed);
+    pl.cw_ctrl = P(w.cw_ctrl);
+    pl.cw_w = P(w.cw_w);
+    pl.cw_proof = P(w.cw_proof);
+    pl.lps = P(w.lps);
+    pl.seed = P(w.seed);
+    pl.peer = P(w.peer);
+    pl.rk_ext = P(w.rk_ext);
+    pl.rk_conv = P(w.rk_conv);
+    pl.sp_onehot = P(w.sp_onehot);
+    pl.sp_payload = P(w.sp_payload);
+    pl.rootsum = P(w.rootsum);
+    pl.beta = P(w.beta);
+    pl.eval_proof = P(w.eval_proof);
+    pl.proof = P(w.proof);
+    pl.qr = P(w.qr);
+    pl.jr = P(w.jr);
+    pl.jr_part = P(w.jr_part);
+    pl.jr_seed = P(w.jr_seed);
+    pl.verifier = P(w.verifier);
+    pl.status = (int32_t*)P(w.status);
+    return pl;
+}
+
+static hipEvent_t get_event(mastic_ctx* c, size_t i) {
+    while (c->ev.size() <= i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev.push_back(e);
+    }
+    return c->ev[i];
+}
+
+
+// ---------------------------------------------------------------- prep_init
+// Parents per wave: enough waves to fill 256 CUs several times over.
+static int choose_ppw(int n_parents, int groups) {
+    long long per = (long long)n_parents * groups / 16384;
+    return (int)std::max(1LL, std::min(per, 64LL));
+}
+
+static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst_off, const uint32_t* src,
+                       size_t src_stride, size_t n, size_t planes) {
+    if (planes == 0) return 0;
+    HIPCHK(c, hipMemcpy2DAsync(dst.as<uint32_t>() + dst_off, dst_stride * 4, src, src_stride * 4, n * 4, planes,
+                               hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+}
+
+template <class F>
+static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
+                     size_t base, int n, int stride, size_t& evi) {
+    const McParams& p = c->p;
+    uint32_t* W = c->work.as<uint32_t>();
+    Planes pl = make_planes(W, wl, n, stride);
+    HIPCHK(c, hipMemsetAsync(W, 0, wl.words * (size_t)stride * 4, c->stream));
+    const size_t ps = mc_public_share_size(p), is = mc_input_share_size(p, agg_id);
+    const uint8_t* ins = agg_id == 0 ? rep->in0.as<uint8_t>() : rep->in1.as<uint8_t>();
+    const PrefixState* pfx = (const PrefixState*)c->pfx.p;
+    hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
+                       rep->nonces.as<uint8_t>() + 16 * base, rep->pub.as<uint8_t>() + ps * base, ins + is * base);
+    hipLaunchKernelGGL(k_setup, dim3((stride + 255) / 256), dim3(256), 0, c->stream, pl, pfx);
+    HIPCHK(c, hipGetLastError());
+
+    const int groups = stride / 64;
+    const int wlw = p.value_len * p.w32;
+    int f_oh = c->pfx_f[PFX_ONEHOT], f_pl = c->pfx_f[PFX_PAYLOAD];
+    auto plane = [&](size_t off) { return W + off * (size_t)stride; };
+    for (int l = 0; l <= t->L; l++) {
+        LevelArgs a;
+        a.level = l;
+        a.last_level = t->L;
+        a.agg_id = agg_id;
+        a.n_parents = t->n_parents[l];
+        a.ppw = choose_ppw(a.n_parents, groups);
+        a.path_bytes = (l + 1 + 7) / 8;
+        a.n_prefixes = t->n_prefixes;
+        a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
+        a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
+        a.child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
+        const int sin = (l + 1) & 1, sout = l & 1;
+        a.fr_seed_in = plane(wl.fr_seed[sin]);
+        a.fr_ctrl_in = plane(wl.fr_ctrl[sin]);
+        a.fr_w_in = plane(wl.fr_w[sin]);
+        a.fr_seed_out = plane(wl.fr_seed[sout]);
+        a.fr_ctrl_out = plane(wl.fr_ctrl[sout]);
+        a.fr_w_out = plane(wl.fr_w[sout]);
+        a.onehot = plane(wl.onehot);
+        a.payload = plane(wl.payload);
+        a.out = plane(wl.out);
+        dim3 grid(groups, (a.n_parents + 4 * a.ppw - 1) / (4 * a.ppw));
+        hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
+        HIPCHK(c, hipEventRecord(e0, c->stream));
+        hipLaunchKernelGGL(k_eval_level<F>, grid, dim3(256), 0, c->stream, p, pl, a, pfx);
+        HIPCHK(c, hipEventRecord(e1, c->stream));
+        HIPCHK(c, hipGetLastError());
+
+        AbsorbArgs ab;
+        ab.seg[0] = a.onehot;
+        ab.nbytes[0] = 2 * a.n_parents * 32;
+        ab.f[0] = f_oh;
+        ab.seg[1] = a.payload;
+        ab.nbytes[1] = l > 0 ? a.n_parents * wlw * 4 : 0;
+        ab.f[1] = f_pl;
+        hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
+        HIPCHK(c, hipEventRecord(e2, c->stream));
+        hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream, pl, ab);
+        HIPCHK(c, hipEventRecord(e3, c->stream));
+        HIPCHK(c, hipGetLastError());
+        f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
+        f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
+    }
+    FinalArgs fa{agg_id, f_oh, f_pl};
+    hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl, fa, pfx);
+    if (t->weight_check) {
+        FlpArgs fl{agg_id, t->L};
+        hipLaunchKernelGGL(k_flp_rand<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl, fl, pfx);
+        hipLaunchKernelGGL(k_flp_query<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl,
+                           flp_consts<F>(p));
+    }
+    HIPCHK(c, hipGetLastError());
+    // results -> the agg_id slot (plane stride = all reports)
+    Result& R = c->res[agg_id];
+    int rc = 0;
+    rc |= copy_planes(c, R.eval_proof, R.stride, base, pl.eval_proof, stride, n, 8);
+    rc |= copy_planes(c, R.status, R.stride, base, (const uint32_t*)pl.status, stride, n, 1);
+    rc |= copy_planes(c, R.out, R.stride, base, plane(wl.out), stride, n,
+                      (size_t)t->n_prefixes * (1 + p.output_len) * p.w32);
+    if (t->weight_check) {
+        rc |= copy_planes(c, R.verifier, R.stride, base, pl.verifier, stride, n, (size_t)p.verifier_len * p.w32);
+        if (p.joint_rand_len > 0) {
+            rc |= copy_planes(c, R.jr_part, R.stride, base, pl.jr_part, stride, n, 8);
+            rc |= copy_planes(c, R.jr_seed, R.stride, base, pl.jr_seed, stride, n, 8);
+        }
+    }
+    return rc;
+}
+
+static uint64_t default_budget(mastic_ctx* c) {
+    if (c->budget) return c->budget;
+    size_t freeb = 0, total = 0;
+    if (hipMemGetInfo(&freeb, &total) != hipSuccess) return 1ull << 30;
+    return (uint64_t)(freeb * 0.45);
+}
+
+extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_t verify_key[32],
+                                const uint8_t* app_ctx, size_t ctx_len, int agg_id, const uint8_t* enc_agg_param,
+                                size_t agg_param_len) {
+    if (!c || !rep || rep->ctx != c) return fail(c, MASTIC_EINVAL, "bad ctx/reports");
+    if (agg_id != 0 && agg_id != 1) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
+    if ((agg_id == 0 && !rep->in0.p) || (agg_id == 1 && !rep->in1.p))
+        return fail(c, MASTIC_EINVAL, "reports hold no input shares for this aggregator");
+    if (!verify_key) return fail(c, MASTIC_EINVAL, "verify key required");
+    Tree* t = nullptr;
+    int rc = build_tree(c, enc_agg_param, agg_param_len, &t);
+    if (rc) return rc;
+    if ((rc = build_prefixes(c, app_ctx, ctx_len, verify_key))) return rc;
+    const McParams& p = c->p;
+    WorkLayout wl = work_layout(p, t);
+    const size_t n = rep->n;
+    Result& R = c->res[agg_id];
+    R.ready = false;
+    R.n = n;
+    R.stride = round_up(std::max<size_t>(n, 1), 64);
+    R.weight_check = t->weight_check;
+    R.n_prefixes = t->n_prefixes;
+    const size_t S = R.stride;
+    if (!R.eval_proof.ensure(S * 8 * 4) || !R.status.ensure(S * 4) ||
+        !R.out.ensure(S * 4 * std::max<size_t>(1, (size_t)t->n_prefixes * (1 + p.output_len) * p.w32)) ||
+        !R.verifier.ensure(S * 4 * (size_t)p.verifier_len * p.w32) || !R.jr_part.ensure(S * 32) ||
+        !R.jr_seed.ensure(S * 32))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (results for %zu reports)", n);
+    HIPCHK(c, hipMemsetAsync(R.jr_part.p, 0, S * 32, c->stream));
+    HIPCHK(c, hipMemsetAsync(R.jr_seed.p, 0, S * 32, c->stream));
+    if (n == 0) {
+        R.ready = true;
+        return 0;
+    }
+    const uint64_t budget = default_budget(c);
+    const size_t per_report = wl.words * 4;
+    size_t chunk = std::min<size_t>(round_up(n, 64), (budget / per_report) / 64 * 64);
+    if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
+    if (!c->work.ensure(per_report * chunk))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * chunk);
+    size_t evi = 0;
+    hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
+    HIPCHK(c, hipEventRecord(t0, c->stream));
+    for (size_t b = 0; b < n; b += chunk) {
+        const int nn = (int)std::min(chunk, n - b);
+        const int stride = (int)round_up(nn, 64);
+        rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi)
+                           : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi);
+        if (rc) return rc;
+    }
+    HIPCHK(c, hipEventRecord(t1, c->stream));
+    c->n_eval = -(int)evi;  // timing pending (resolved by mastic_last_timing)
+    R.ready = true;
+    return 0;
+}
+
+static void put_words(uint8_t* dst, const std::vector<uint32_t>& planes, size_t stride, size_t r, size_t first,
+                      size_t count) {
+    for (size_t k = 0; k < count; k++) {
+        uint32_t w = planes[(first + k) * stride + r];
+        dst[4 * k] = (uint8_t)w;
+        dst[4 * k + 1] = (uint8_t)(w >> 8);
+        dst[4 * k + 2] = (uint8_t)(w >> 16);
+        dst[4 * k + 3] = (uint8_t)(w >> 24);
+    }
+}
+
+static int fetch(mastic_ctx* c, const DevBuf& b, size_t planes, size_t stride, std::vector<uint32_t>& out) {
+    out.resize(planes * stride);
+    if (planes == 0) return 0;
+    HIPCHK(c, hipMemcpy(out.data(), b.p, planes * stride * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_shares, uint8_t* jr_seeds,
+                                  uint8_t* out_shares, int32_t* status) {
+    if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
+    Result& R = c->res[agg_id];
+    if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const McParams& p = c->p;
+    const size_t n = R.n, S = R.stride;
+    if (n == 0) return 0;
+    std::vector<uint32_t> ep, ver, jp, js, st, out;
+    int rc = 0;
+    if (prep_shares) {
+        rc |= fetch(c, R.eval_proof, 8, S, ep);
+        if (R.weight_check) {
+            rc |= fetch(c, R.verifier, (size_t)p.verifier_len * p.w32, S, ver);
+            if (p.joint_rand_len > 0) rc |= fetch(c, R.jr_part, 8, S, jp);
+        }
+        if (rc) return rc;
+        const size_t psz = mc_prep_share_size(p, R.weight_check);
+        for (size_t r = 0; r < n; r++) {
+            uint8_t* d = prep_shares + psz * r;
+            put_words(d, ep, S, r, 0, 8);
+            d += 32;
+            if (R.weight_check) {
+                if (p.joint_rand_len > 0) {
+                    put_words(d, jp, S, r, 0, 8);
+                    d += 32;
+                }
+                put_words(d, ver, S, r, 0, (size_t)p.verifier_len * p.w32);
+            }
+        }
+    }
+    if (jr_seeds) {
+        if ((rc = fetch(c, R.jr_seed, 8, S, js))) return rc;
+        for (size_t r = 0; r < n; r++) put_words(jr_seeds + 32 * r, js, S, r, 0, 8);
+    }
+    if (out_shares) {
+        const size_t ow = (size_t)R.n_prefixes * (1 + p.output_len) * p.w32;
+        if ((rc = fetch(c, R.out, ow, S, out))) return rc;
+        for (size_t r = 0; r < n; r++) put_words(out_shares + 4 * ow * r, out, S, r, 0, ow);
+    }
+    if (status) {
+        if ((rc = fetch(c, R.status, 1, S, st))) return rc;
+        for (size_t r = 0; r < n; r++) status[r] = (int32_t)st[r];
+    }
+    return 0;
+}
+
+extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid, uint8_t* agg_share) {
+    if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
+    Result& R = c->res[agg_id];
+    if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
+    const McParams& p = c->p;
+    const size_t rows = (size_t)R.n_prefixes * (1 + p.output_len);
+    static thread_local DevBuf dvalid, dagg;
+    const uint8_t* dv = nullptr;
+    if (valid && R.n) {
+        if (!dvalid.ensure(R.n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        HIPCHK(c, hipMemcpyAsync(dvalid.p, valid, R.n, hipMemcpyHostToDevice, c->stream));
+        dv = dvalid.as<uint8_t>();
+    }
+    if (!dagg.ensure(std::max<size_t>(rows, 1) * p.w32 * 4)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+    if (rows) {
+        if (p.field == 64)
+            hipLaunchKernelGGL(k_fold<F64>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
+                               (int)R.stride, dv, dagg.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_fold<F128>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
+                               (int)R.stride, dv, dagg.as<uint32_t>());
+        HIPCHK(c, hipGetLastError());
+    }
+    if (agg_share && rows) HIPCHK(c, hipMemcpyAsync(agg_share, dagg.p, rows * p.w32 * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int mastic_synchronize(mastic_ctx* c) {
+    if (!c) return MASTIC_EINVAL;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int mastic_last_timing(mastic_ctx* c, double* eval_ms, int* eval_launches, double* absorb_ms,
+                                  int* absorb_launches, double* total_ms) {
+    if (!c) return MASTIC_EINVAL;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->n_eval < 0) {
+        const size_t evi = (size_t)(-c->n_eval);
+        double te = 0, ta = 0;
+        int ne = 0, na = 0;
+        float ms = 0;
+        // events: [t0, t1] then per level [e0, e1, e2, e3]
+        for (size_t i = 2; i + 3 < evi + 1 && i + 3 <= evi - 1 + 1; i += 4) {
+            if (i + 3 >= evi) break;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+            te += ms;
+            ne++;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i + 2], c->ev[i + 3]));
+            ta += ms;
+            na++;
+        }
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->t_total = ms;
+        c->t_eval = te;
+        c->t_absorb = ta;
+        c->n_eval = ne;
+        c->n_absorb = na;
+    }
+    if (eval_ms) *eval_ms = c->t_eval;
+    if (eval_launches) *eval_launches = c->n_eval;
+    if (absorb_ms) *absorb_ms = c->t_absorb;
+    if (absorb_launches) *absorb_launches = c->n_absorb;
+    if (total_ms) *total_ms = c->t_total;
+    return 0;
+}
+
+extern "C" int mastic_tree_stats(mastic_ctx* c, const uint8_t* enc, size_t len, uint64_t* nodes, uint64_t* interior,
+                                 uint64_t* max_level_nodes) {
+    Tree* t = nullptr;
+    int rc = build_tree(c, enc, len, &t);
+    if (rc) return rc;
+    if (nodes) *nodes = t->nodes;
+    if (interior) *interior = t->interior;
+    if (max_level_nodes) *max_level_nodes = (uint64_t)t->max_level_nodes;
+    return 0;
+}
+
+extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t verify_key[32], const uint8_t* app_ctx,
+                                      size_t ctx_len, int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len,
+                                      size_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                                      const uint8_t* input_shares, uint8_t* prep_shares_out, uint8_t* jr_seeds_out,
+                                      uint8_t* out_shares_out, int32_t* status_out) {
+    if (!c) return MASTIC_EINVAL;
+    if (agg_id != 0 && agg_id != 1) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
+    mastic_reports* rep = nullptr;
+    int rc = mastic_reports_create(c, n, &rep);
+    if (rc) return rc;
+    rc = mastic_reports_upload(rep, nonces, public_shares, agg_id == 0 ? input_shares : nullptr,
+                               agg_id == 1 ? input_shares : nullptr);
+    if (!rc) rc = mastic_prep_init(c, rep, verify_key, app_ctx, ctx_len, agg_id, enc_agg_param, agg_param_len);
+    if (!rc) rc = mastic_prep_result(c, agg_id, prep_shares_out, jr_seeds_out, out_shares_out, status_out);
+    mastic_reports_destroy(rep);
+    return rc;
+}
+
+// ---------------------------------------------------------------- decide
+extern "C" int mastic_decide_batch(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* enc,
+                                   size_t len, size_t n, const uint8_t* ps0, const uint8_t* ps1, uint8_t* msgs_out,
+                                   uint8_t* valid_out) {
+    if (!c) return MASTIC_EINVAL;
+    Tree* t = nullptr;
+    int rc = build_tree(c, enc, len, &t);
+    if (rc) return rc;
+    if (n == 0) return 0;
+    if ((rc = build_prefixes(c, app_ctx, ctx_len, nullptr))) return rc;
+    const McParams& p = c->p;
+    const size_t psz = mc_prep_share_size(p, t->weight_check);
+    const size_t stride = round_up(n, 64);
+    DevBuf a, b, ver, msg, st;
+    if (!a.ensure(psz * n) || !b.ensure(psz * n) || !ver.ensure(stride * 4 * (size_t)p.verifier_len * p.w32) ||
+        !msg.ensure(32 * n) || !st.ensure(n))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (decide)");
+    HIPCHK(c, hipMemcpyAsync(a.p, ps0, psz * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(b.p, ps1, psz * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(msg.p, 0, 32 * n, c->stream));
+    if (p.field == 64)
+        hipLaunchKernelGGL(k_decide<F64>, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, (int)n, (int)stride,
+                           (int)t->weight_check, a.as<uint8_t>(), b.as<uint8_t>(), (int)psz, ver.as<uint32_t>(),
+                           (const PrefixState*)c->pfx.p, msg.as<uint8_t>(), st.as<uint8_t>());
+    else
+        hipLaunchKernelGGL(k_decide<F128>, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, (int)n, (int)stride,
+                           (int)t->weight_check, a.as<uint8_t>(), b.as<uint8_t>(), (int)psz, ver.as<uint32_t>(),
+                           (const PrefixState*)c->pfx.p, msg.as<uint8_t>(), st.as<uint8_t>());
+    HIPCHK(c, hipGetLastError());
+    if (msgs_out && t->weight_check && p.joint_rand_len > 0)
+        HIPCHK(c, hipMemcpyAsync(msgs_out, msg.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
+    if (valid_out) HIPCHK(c, hipMemcpyAsync(valid_out, st.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------- reports
+extern "C" int mastic_reports_create(mastic_ctx* c, size_t n, mastic_reports** out) {
+    if (!c || !out) return MASTIC_EINVAL;
+    mastic_reports* r = new mastic_reports();
+    r->ctx = c;
+    r->n = n;
+    const McParams& p = c->p;
+    if (!r->nonces.ensure(16 * n) || !r->pub.ensure((size_t)mc_public_share_size(p) * n)) {
+        delete r;
+        return fail(c, MASTIC_ENOMEM, "out of device memory (reports)");
+    }
+    *out = r;
+    return 0;
+}
+
+extern "C" void mastic_reports_destroy(mastic_reports* r) { delete r; }
+extern "C" size_t mastic_reports_count(const mastic_reports* r) { return r ? r->n : 0; }
+
+extern "C" int mastic_reports_upload(mastic_reports* r, const uint8_t* nonces, const uint8_t* pub,
+                                     const uint8_t* in0, const uint8_t* in1) {
+    if (!r) return MASTIC_EINVAL;
+    mastic_ctx* c = r->ctx;
+    const McParams& p = c->p;
+    const size_t n = r->n;
+    if (nonces) HIPCHK(c, hipMemcpy(r->nonces.p, nonces, 16 * n, hipMemcpyHostToDevice));
+    if (pub) HIPCHK(c, hipMemcpy(r->pub.p, pub, (size_t)mc_public_share_size(p) * n, hipMemcpyHostToDevice));
+    if (in0) {
+        if (!r->in0.ensure((size_t)mc_input_share_size(p, 0) * n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        HIPCHK(c, hipMemcpy(r->in0.p, in0, (size_t)mc_input_share_size(p, 0) * n, hipMemcpyHostToDevice));
+    }
+    if (in1) {
+        if (!r->in1.ensure((size_t)mc_input_share_size(p, 1) * n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        HIPCHK(c, hipMemcpy(r->in1.p, in1, (size_t)mc_input_share_size(p, 1) * n, hipMemcpyHostToDevice));
+    }
+    return 0;
+}
+
+extern "C" int mastic_reports_download(mastic_reports* r, uint8_t* nonces, uint8_t* pub, uint8_t* in0, uint8_t* in1) {
+    if (!r) return MASTIC_EINVAL;
+    mastic_ctx* c = r->ctx;
+    const McParams& p = c->p;
+    const size_t n = r->n;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nonces) HIPCHK(c, hipMemcpy(nonces, r->nonces.p, 16 * n, hipMemcpyDeviceToHost));
+    if (pub) HIPCHK(c, hipMemcpy(pub, r->pub.p, (size_t)mc_public_share_size(p) * n, hipMemcpyDeviceToHost));
+    if (in0) {
+        if (!r->in0.p) return fail(c, MASTIC_EINVAL, "no leader input shares");
+        HIPCHK(c, hipMemcpy(in0, r->in0.p, (size_t)mc_input_share_size(p, 0) * n, hipMemcpyDeviceToHost));
+    }
+    if (in1) {
+        if (!r->in1.p) return fail(c, MASTIC_EINVAL, "no helper input shares");
+        HIPCHK(c, hipMemcpy(in1, r->in1.p, (size_t)mc_input_share_size(p, 1) * n, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+template <class F>
+static int shard_impl(mastic_ctx* c, mastic_reports* rep, const uint8_t* alphas, const uint8_t* betas,
+                      const uint8_t* nonces, const uint8_t* rands) {
+    typedef typename F::E E;
+    const McParams& p = c->p;
+    const size_t n = rep->n;
+    const size_t ab = (p.bits + 7) / 8, bsz = (size_t)p.meas_len * p.enc, rs = mc_rand_size(p);
+    if (!rep->in0.ensure((size_t)mc_input_share_size(p, 0) * n) || !rep->in1.ensure((size_t)mc_input_share_size(p, 1) * n))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (input shares)");
+    DevBuf da, db, dr, tab;
+    if (!da.ensure(ab * n) || !db.ensure(bsz * n) || !dr.ensure(rs * n) || !tab.ensure(sizeof(E) * p.P))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (shard inputs)");
+    HIPCHK(c, hipMemcpy(da.p, alphas, ab * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(db.p, betas, bsz * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(dr.p, rands, rs * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(rep->nonces.p, nonces, 16 * n, hipMemcpyHostToDevice));
+    FlpConsts<F> fc = flp_consts<F>(p);
+    std::vector<E> pows(p.P);
+    E ainv = finv<F>(fc.alpha), acc = F::from_u64(1);
+    for (int i = 0; i < p.P; i++) {
+        pows[i] = acc;
+        acc = F::mul(acc, ainv);
+    }
+    HIPCHK(c, hipMemcpy(tab.p, pows.data(), sizeof(E) * p.P, hipMemcpyHostToDevice));
+    // scratch planes per report
+    const size_t wl = (size_t)p.value_len * p.w32;
+    const size_t words = wl + 88 + 2 * wl + (size_t)std::max(1, p.joint_rand_len) * p.w32 + (size_t)p.arity * p.w32 +
+                         2 * (size_t)p.arity * p.P * p.w32 + 2 * (size_t)p.proof_len * p.w32 + 32;
+    const uint64_t budget = default_budget(c);
+    size_t chunk = std::min<size_t>(round_up(n, 64), std::max<size_t>(64, (budget / (words * 4)) / 64 * 64));
+    DevBuf scratch;
+    if (!scratch.ensure(words * 4 * chunk)) return fail(c, MASTIC_ENOMEM, "out of device memory (shard scratch)");
+    for (size_t b = 0; b < n; b += chunk) {
+        const int nn = (int)std::min(chunk, n - b);
+        const int S = (int)round_up(nn, 64);
+        ShardArgs a;
+        a.n = nn;
+        a.stride = S;
+        a.alphas = da.as<uint8_t>() + ab * b;
+        a.betas = db.as<uint8_t>() + bsz * b;
+        a.nonces = rep->nonces.as<uint8_t>() + 16 * b;
+        a.rands = dr.as<uint8_t>() + rs * b;
+        a.pub = rep->pub.as<uint8_t>() + (size_t)mc_public_share_size(p) * b;
+        a.in0 = rep->in0.as<uint8_t>() + (size_t)mc_input_share_size(p, 0) * b;
+        a.in1 = rep->in1.as<uint8_t>() + (size_t)mc_input_share_size(p, 1) * b;
+        uint32_t* w = scratch.as<uint32_t>();
+        size_t o = 0;
+        auto take = [&](size_t k) {
+            uint32_t* r = w + o * S;
+            o += k;
+            return r;
+        };
+        a.beta = take(wl);
+        a.rke = take(44);
+        a.rkc = take(44);
+        a.bs = take(2 * wl);
+        a.jr = take((size_t)std::max(1, p.joint_rand_len) * p.w32);
+        a.prand = take((size_t)p.arity * p.w32);
+        a.vals = take((size_t)p.arity * p.P * p.w32);
+        a.coef = take((size_t)p.arity * p.P * p.w32);
+        a.proof = take((size_t)p.proof_len * p.w32);
+        a.hps = take((size_t)p.proof_len * p.w32);
+        a.misc = take(32);
+        hipLaunchKernelGGL(k_shard<F>, dim3((nn + 255) / 256), dim3(256), 0, c->stream, p, a,
+                           (const PrefixState*)c->pfx.p, fc, tab.as<E>());
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx, size_t ctx_len,
+                                    const uint8_t* alphas, const uint8_t* betas, const uint8_t* nonces,
+                                    const uint8_t* rands) {
+    if (!rep) return MASTIC_EINVAL;
+    mastic_ctx* c = rep->ctx;
+    if (rep->n == 0) return 0;
+    if (!alphas || !nonces || !rands || (!betas && c->p.meas_len > 0)) return fail(c, MASTIC_EINVAL, "null input");
+    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr);
+    if (rc) return rc;
+    return c->p.field == 64 ? shard_impl<F64>(c, rep, alphas, betas, nonces, rands)
+                            : shard_impl<F128>(c, rep, alphas, betas, nonces, rands);
+}
+
+extern "C" int mastic_shard_batch(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, size_t n,
+                                  const uint8_t* alphas, const uint8_t* betas, const uint8_t* nonces,
+                                  const uint8_t* rands, uint8_t* pub_out, uint8_t* in0_out, uint8_t* in1_out) {
+    if (!c) return MASTIC_EINVAL;
+    mastic_reports* rep = nullptr;
+    int rc = mastic_reports_create(c, n, &rep);
+    if (rc) return rc;
+    rc = mastic_reports_shard(rep, app_ctx, ctx_len, alphas, betas, nonces, rands);
+    if (!rc) rc = mastic_reports_download(rep, nullptr, pub_out, in0_out, in1_out);
+    mastic_reports_destroy(rep);
+    return rc;
+}
+
+// ---------------------------------------------------------------- ctx
+extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
+    if (!up || !out) return MASTIC_EINVAL;
+    *out = nullptr;
+    McParams p;
+    if (mc_derive((int)up->circuit, (int)up->bits, (int)up->length, (int)up->sum_vec_bits, up->max_measurement,
+                  (int)up->chunk_length, &p))
+        return MASTIC_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MASTIC_ENODEV;
+    if (up->device < 0 || up->device >= ndev) return MASTIC_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, up->device) != hipSuccess) return MASTIC_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MASTIC_ENODEV;
+    if (hipSetDevice(up->device) != hipSuccess) return MASTIC_ENODEV;
+    mastic_ctx* c = new mastic_ctx();
+    c->user = *up;
+    c->p = p;
+    c->device = up->device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return MASTIC_EHIP;
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" void mastic_ctx_destroy(mastic_ctx* c) {
+    if (!c) return;
+    (void)hipStreamSynchronize(c->stream);
+    delete c;
+}
+
+extern "C" const char* mastic_last_error(const mastic_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+extern "C" int mastic_set_memory_budget(mastic_ctx* c, uint64_t bytes) {
+    if (!c) return MASTIC_EINVAL;
+    c->budget = bytes;
+    return 0;
+}
+
+extern "C" int mastic_get_sizes(const mastic_ctx* c, mastic_sizes* s) {
+    if (!c || !s) return MASTIC_EINVAL;
+    const McParams& p = c->p;
+    s->field_bytes = p.enc;
+    s->value_len = p.value_len;
+    s->meas_len = p.meas_len;
+    s->output_len = p.output_len;
+    s->proof_len = p.proof_len;
+    s->verifier_len = p.verifier_len;
+    s->joint_rand_len = p.joint_rand_len;
+    s->query_rand_len = p.query_rand_len;
+    s->prove_rand_len = p.prove_rand_len;
+    s->rand_size = mc_rand_size(p);
+    s->public_share_size = mc_public_share_size(p);
+    s->input_share_size[0] = mc_input_share_size(p, 0);
+    s->input_share_size[1] = mc_input_share_size(p, 1);
+    s->prep_share_size[0] = mc_prep_share_size(p, false);
+    s->prep_share_size[1] = mc_prep_share_size(p, true);
+    s->algorithm_id = p.alg_id;
+    return 0;
+}

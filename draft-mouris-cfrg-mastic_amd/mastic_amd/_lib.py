@@ -1,0 +1,140 @@
+"""ctypes binding of libmastic_hip.so (the C ABI declared in include/mastic_hip.h).
+
+There is no fallback: if the shared library is missing or no gfx950 device is
+present, every entry point raises.  ``build()`` compiles the library in-tree
+with hipcc for gfx950.
+"""
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(PKG_DIR)
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+LIB_PATH = os.path.join(PKG_DIR, "libmastic_hip.so")
+
+MASTIC_OK = 0
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -5: "EHIP"}
+
+# Every symbol include/mastic_hip.h declares (checked by tests/test_boundary.py).
+EXPORTS = [
+    "mastic_ctx_create", "mastic_ctx_destroy", "mastic_last_error", "mastic_get_sizes",
+    "mastic_set_memory_budget", "mastic_reports_create", "mastic_reports_destroy",
+    "mastic_reports_count", "mastic_reports_upload", "mastic_reports_download",
+    "mastic_reports_shard", "mastic_prep_init", "mastic_prep_result", "mastic_aggregate",
+    "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
+    "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats",
+]
+
+
+class MasticParams(ctypes.Structure):
+    _fields_ = [
+        ("circuit", ctypes.c_uint32),
+        ("bits", ctypes.c_uint32),
+        ("length", ctypes.c_uint32),
+        ("sum_vec_bits", ctypes.c_uint32),
+        ("max_measurement", ctypes.c_uint64),
+        ("chunk_length", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+    ]
+
+
+class MasticSizes(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_uint32) for name in (
+        "field_bytes", "value_len", "meas_len", "output_len", "proof_len", "verifier_len",
+        "joint_rand_len", "query_rand_len", "prove_rand_len", "rand_size", "public_share_size")] + [
+        ("input_share_size", ctypes.c_uint32 * 2),
+        ("prep_share_size", ctypes.c_uint32 * 2),
+        ("algorithm_id", ctypes.c_uint32),
+    ]
+
+
+class MasticError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%s)" % (msg, ERRORS.get(code, code)))
+        self.code = code
+
+
+def build(verbose=False, force=False) -> str:
+    """Compile csrc/mastic_hip.hip for gfx950 into the package directory."""
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    srcs.append(os.path.join(INCLUDE, "mastic_hip.h"))
+    newest = max(os.path.getmtime(s) for s in srcs)
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
+        return LIB_PATH
+    tmp = LIB_PATH + ".%d.tmp" % os.getpid()
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I" + INCLUDE, "-o", tmp, os.path.join(CSRC, "mastic_hip.hip")]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError("libmastic_hip.so is not built (run __graft_entry__.build()); "
+                                      "the HIP path has no CPU fallback")
+                l = ctypes.CDLL(LIB_PATH)
+                P = ctypes.c_void_p
+                u8p = ctypes.c_char_p
+                sz = ctypes.c_size_t
+                i32 = ctypes.c_int
+                sig = {
+                    "mastic_ctx_create": (i32, [ctypes.POINTER(MasticParams), ctypes.POINTER(P)]),
+                    "mastic_ctx_destroy": (None, [P]),
+                    "mastic_last_error": (ctypes.c_char_p, [P]),
+                    "mastic_get_sizes": (i32, [P, ctypes.POINTER(MasticSizes)]),
+                    "mastic_set_memory_budget": (i32, [P, ctypes.c_uint64]),
+                    "mastic_reports_create": (i32, [P, sz, ctypes.POINTER(P)]),
+                    "mastic_reports_destroy": (None, [P]),
+                    "mastic_reports_count": (sz, [P]),
+                    "mastic_reports_upload": (i32, [P, P, P, P, P]),
+                    "mastic_reports_download": (i32, [P, P, P, P, P]),
+                    "mastic_reports_shard": (i32, [P, u8p, sz, P, P, P, P]),
+                    "mastic_prep_init": (i32, [P, P, u8p, u8p, sz, i32, u8p, sz]),
+                    "mastic_prep_result": (i32, [P, i32, P, P, P, P]),
+                    "mastic_aggregate": (i32, [P, i32, P, P]),
+                    "mastic_synchronize": (i32, [P]),
+                    "mastic_prep_init_batch": (i32, [P, u8p, u8p, sz, i32, u8p, sz, sz, P, P, P, P, P, P, P]),
+                    "mastic_decide_batch": (i32, [P, u8p, sz, u8p, sz, sz, P, P, P, P]),
+                    "mastic_shard_batch": (i32, [P, u8p, sz, sz, P, P, P, P, P, P, P]),
+                    "mastic_last_timing": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_double)]),
+                    "mastic_tree_stats": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+                }
+                for name, (res, args) in sig.items():
+                    fn = getattr(l, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = l
+    return _lib
+
+
+def buf(data) -> ctypes.c_void_p:
+    """Pointer to the bytes of a bytes/bytearray/numpy array (None -> NULL)."""
+    if data is None:
+        return None
+    import numpy as np
+    if isinstance(data, np.ndarray):
+        assert data.flags["C_CONTIGUOUS"]
+        return ctypes.c_void_p(data.ctypes.data)
+    if isinstance(data, bytearray):
+        return ctypes.c_void_p(ctypes.addressof((ctypes.c_char * len(data)).from_buffer(data)))
+    if isinstance(data, bytes):
+        return ctypes.cast(ctypes.c_char_p(data), ctypes.c_void_p)
+    raise TypeError(type(data))

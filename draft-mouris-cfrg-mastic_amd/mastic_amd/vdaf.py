@@ -1,0 +1,470 @@
+"""Mastic VDAF on MI355X — the drop-in for the reference's ``Mastic`` class.
+
+Mirrors ``poc/mastic.py`` (class ``Mastic`` :52-559, instantiations
+:567-614): same method names, argument meaning, return types and error
+behaviour (``ValueError`` for malformed inputs, ``Exception`` for failed
+verification).  The per-report methods are batches of one; the ``*_batch``
+methods are the production path and keep everything in wire encodings
+(``test_vec/mastic`` format).  All cryptography runs in the HIP kernels
+behind ``libmastic_hip.so``; this module only (de)serialises.
+"""
+import ctypes
+import itertools
+
+import numpy as np
+
+from . import _lib
+from .field import Field64, Field128
+
+PROOF_SIZE = 32
+CIRCUIT_IDS = {"Count": 1, "Sum": 2, "SumVec": 3, "Histogram": 4, "MultihotCountVec": 5}
+
+
+def _check(ctx_ptr, rc):
+    if rc != 0:
+        msg = _lib.lib().mastic_last_error(ctx_ptr) if ctx_ptr else b""
+        text = (msg or b"").decode(errors="replace") or "mastic error"
+        if rc == -22:
+            raise ValueError(text)
+        raise _lib.MasticError(rc, text)
+
+
+def _pack_path(path) -> bytes:
+    """MSB-first bit packing (PrefixTreeIndex.encode, poc/vidpf.py:33-39)."""
+    out = bytearray((len(path) + 7) // 8)
+    for (i, b) in enumerate(path):
+        out[i // 8] |= int(bool(b)) << (7 - i % 8)
+    return bytes(out)
+
+
+def _pack_bits_lsb(bits) -> bytes:
+    out = bytearray((len(bits) + 7) // 8)
+    for (i, b) in enumerate(bits):
+        out[i // 8] |= int(bool(b)) << (i % 8)
+    return bytes(out)
+
+
+class Mastic:
+    """Mastic(bits, valid) with the validity circuit given as (name, params)."""
+
+    ID = 0xFFFFFFFF
+    VERIFY_KEY_SIZE = 32
+    NONCE_SIZE = 16
+    SHARES = 2
+    ROUNDS = 1
+    test_vec_name = "Mastic"
+
+    def __init__(self, bits: int, circuit: str, length: int = 0, sum_vec_bits: int = 0,
+                 max_measurement: int = 0, chunk_length: int = 0, device: int = 0):
+        self.circuit = circuit
+        self.params = _lib.MasticParams(CIRCUIT_IDS[circuit], bits, length, sum_vec_bits,
+                                        max_measurement, chunk_length, device)
+        self._ctx = ctypes.c_void_p()
+        rc = _lib.lib().mastic_ctx_create(ctypes.byref(self.params), ctypes.byref(self._ctx))
+        if rc != 0:
+            raise _lib.MasticError(rc, "mastic_ctx_create failed (needs an MI355X / gfx950 device; "
+                                       "there is no CPU fallback)")
+        sz = _lib.MasticSizes()
+        _check(self._ctx, _lib.lib().mastic_get_sizes(self._ctx, ctypes.byref(sz)))
+        self.sizes = sz
+        self.field = Field64 if sz.field_bytes == 8 else Field128
+        self.BITS = bits
+        self.VALUE_LEN = sz.value_len
+        self.MEAS_LEN = sz.meas_len
+        self.OUTPUT_LEN = sz.output_len
+        self.PROOF_LEN = sz.proof_len
+        self.VERIFIER_LEN = sz.verifier_len
+        self.JOINT_RAND_LEN = sz.joint_rand_len
+        self.RAND_SIZE = sz.rand_size
+        self.ID = sz.algorithm_id
+        self.length = length
+        self.sum_vec_bits = sum_vec_bits
+        self.max_measurement = max_measurement
+        self.chunk_length = chunk_length
+        if circuit == "Sum":
+            self._wbits = max_measurement.bit_length()
+            self._offset = 2 ** self._wbits - 1 - max_measurement
+        elif circuit == "MultihotCountVec":
+            self._wbits = max_measurement.bit_length()
+            self._offset = 2 ** self._wbits - 1 - max_measurement
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx:
+            _lib.lib().mastic_ctx_destroy(ctx)
+            self._ctx = None
+
+    # ------------------------------------------------------------ circuits
+    def encode_measurement(self, weight):
+        """Valid.encode (vdaf_poc.flp_bbcggi19) -> MEAS_LEN field elements."""
+        F = self.field
+        c = self.circuit
+        if c == "Count":
+            return [F(int(weight))]
+        if c == "Sum":
+            if not 0 <= weight <= self.max_measurement:
+                raise ValueError("measurement out of range")
+            return (F.encode_into_bit_vector(weight, self._wbits)
+                    + F.encode_into_bit_vector(weight + self._offset, self._wbits))
+        if c == "SumVec":
+            if len(weight) != self.length:
+                raise ValueError("incorrect measurement length")
+            return [x for v in weight for x in F.encode_into_bit_vector(int(v), self.sum_vec_bits)]
+        if c == "Histogram":
+            if not 0 <= weight < self.length:
+                raise ValueError("bucket out of range")
+            return [F(int(i == weight)) for i in range(self.length)]
+        if len(weight) != self.length:
+            raise ValueError("incorrect measurement length")
+        total = sum(int(bool(x)) for x in weight)
+        if total > self.max_measurement:
+            raise ValueError("measurement weight too large")
+        return [F(int(bool(x))) for x in weight] + F.encode_into_bit_vector(self._offset + total, self._wbits)
+
+    def decode_result(self, output, num_measurements):
+        """Valid.decode."""
+        if self.circuit in ("Count", "Sum"):
+            return output[0].int()
+        return [x.int() for x in output]
+
+    # --------------------------------------------------------- wire sizes
+    def public_share_size(self):
+        return self.sizes.public_share_size
+
+    def input_share_size(self, agg_id):
+        return self.sizes.input_share_size[agg_id]
+
+    def prep_share_size(self, weight_check):
+        return self.sizes.prep_share_size[1 if weight_check else 0]
+
+    # ------------------------------------------------------ batch (native)
+    def shard_batch(self, ctx: bytes, alphas, weights, nonces: bytes, rands: bytes):
+        """Client shard of n reports on the GPU.  Returns the wire encodings
+        (public_shares, input_shares_0, input_shares_1) as bytes."""
+        n = len(alphas)
+        ab = (self.BITS + 7) // 8
+        a = bytearray(ab * n)
+        for (i, alpha) in enumerate(alphas):
+            if len(alpha) != self.BITS:
+                raise ValueError("alpha out of range")
+            a[ab * i: ab * (i + 1)] = _pack_path(alpha)
+        betas = b"".join(self.field.encode_vec(self.encode_measurement(w)) for w in weights)
+        return self.shard_encoded(ctx, n, bytes(a), betas, nonces, rands)
+
+    def shard_encoded(self, ctx: bytes, n: int, alphas: bytes, betas: bytes, nonces: bytes, rands: bytes):
+        if len(nonces) != 16 * n or len(rands) != self.RAND_SIZE * n:
+            raise ValueError("nonce / randomness has incorrect length")
+        pub = np.empty(self.sizes.public_share_size * n, np.uint8)
+        in0 = np.empty(self.sizes.input_share_size[0] * n, np.uint8)
+        in1 = np.empty(self.sizes.input_share_size[1] * n, np.uint8)
+        _check(self._ctx, _lib.lib().mastic_shard_batch(
+            self._ctx, ctx, len(ctx), n, _lib.buf(alphas), _lib.buf(betas), _lib.buf(nonces),
+            _lib.buf(rands), _lib.buf(pub), _lib.buf(in0), _lib.buf(in1)))
+        return (pub.tobytes(), in0.tobytes(), in1.tobytes())
+
+    def prep_init_batch(self, verify_key: bytes, ctx: bytes, agg_id: int, agg_param, nonces: bytes,
+                        public_shares: bytes, input_shares: bytes, want_out_shares=True):
+        """prep_init for n reports (wire in, wire out).  Returns
+        (prep_shares bytes, jr_seeds bytes, out_shares bytes or None, status int32 array)."""
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        (level, count, wc) = self._agg_param_header(enc)
+        n = len(nonces) // 16
+        if len(verify_key) != self.VERIFY_KEY_SIZE:
+            raise ValueError("verify key has incorrect length")
+        if len(public_shares) != n * self.sizes.public_share_size:
+            raise ValueError("public shares have incorrect length")
+        if len(input_shares) != n * self.sizes.input_share_size[agg_id]:
+            raise ValueError("input shares have incorrect length")
+        ps = np.empty(n * self.prep_share_size(wc), np.uint8)
+        js = np.empty(n * 32, np.uint8)
+        ow = count * (1 + self.OUTPUT_LEN) * self.field.ENCODED_SIZE
+        out = np.empty(n * ow, np.uint8) if want_out_shares else None
+        st = np.empty(n, np.int32)
+        _check(self._ctx, _lib.lib().mastic_prep_init_batch(
+            self._ctx, verify_key, ctx, len(ctx), agg_id, enc, len(enc), n, _lib.buf(nonces),
+            _lib.buf(public_shares), _lib.buf(input_shares), _lib.buf(ps), _lib.buf(js), _lib.buf(out),
+            _lib.buf(st)))
+        return (ps.tobytes(), js.tobytes(), None if out is None else out.tobytes(), st)
+
+    def decide_batch(self, ctx: bytes, agg_param, prep_shares_0: bytes, prep_shares_1: bytes):
+        """prep_shares_to_prep for n report pairs -> (prep_msgs bytes, status uint8 array)."""
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        (_level, _count, wc) = self._agg_param_header(enc)
+        psz = self.prep_share_size(wc)
+        n = len(prep_shares_0) // psz
+        if len(prep_shares_0) != n * psz or len(prep_shares_1) != n * psz:
+            raise ValueError("prep shares have incorrect length")
+        msgs = np.zeros(32 * n, np.uint8)
+        valid = np.empty(n, np.uint8)
+        _check(self._ctx, _lib.lib().mastic_decide_batch(
+            self._ctx, ctx, len(ctx), enc, len(enc), n, _lib.buf(prep_shares_0), _lib.buf(prep_shares_1),
+            _lib.buf(msgs), _lib.buf(valid)))
+        return (msgs.tobytes(), valid)
+
+    def aggregate_device(self, agg_id: int, agg_param, valid=None):
+        """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU."""
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        (_level, count, _wc) = self._agg_param_header(enc)
+        out = np.empty(count * (1 + self.OUTPUT_LEN) * self.field.ENCODED_SIZE, np.uint8)
+        v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
+        _check(self._ctx, _lib.lib().mastic_aggregate(self._ctx, agg_id, _lib.buf(v), _lib.buf(out)))
+        return self.field.decode_vec(out.tobytes())
+
+    def tree_stats(self, agg_param):
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._ctx, _lib.lib().mastic_tree_stats(self._ctx, enc, len(enc), ctypes.byref(a),
+                                                       ctypes.byref(b), ctypes.byref(c)))
+        return (a.value, b.value, c.value)
+
+    @staticmethod
+    def _agg_param_header(enc: bytes):
+        if len(enc) < 7:
+            raise ValueError("agg param too short")
+        return (int.from_bytes(enc[:2], "big"), int.from_bytes(enc[2:6], "big"), bool(enc[-1]))
+
+    # ------------------------------------------- reference API (one report)
+    def shard(self, ctx, measurement, nonce, rand):
+        """poc/mastic.py:91-185"""
+        if len(nonce) != self.NONCE_SIZE:
+            raise ValueError("incorrect nonce size")
+        if len(rand) != self.RAND_SIZE:
+            raise ValueError("randomness has incorrect length")
+        (alpha, weight) = measurement
+        (pub, in0, in1) = self.shard_batch(ctx, [alpha], [weight], nonce, rand)
+        return (self.decode_public_share(pub), [self.decode_input_share(0, in0), self.decode_input_share(1, in1)])
+
+    def is_valid(self, agg_param, previous_agg_params) -> bool:
+        """poc/mastic.py:187-203"""
+        (level, _prefixes, do_weight_check) = agg_param
+        weight_checked = ((do_weight_check and len(previous_agg_params) == 0)
+                          or (not do_weight_check and any(p[2] for p in previous_agg_params)))
+        level_increased = len(previous_agg_params) == 0 or level > previous_agg_params[-1][0]
+        return weight_checked and level_increased
+
+    def prep_init(self, verify_key, ctx, agg_id, agg_param, nonce, public_share, input_share):
+        """poc/mastic.py:205-318 (routed to the GPU as a batch of one)."""
+        if agg_id not in (0, 1):
+            raise ValueError("invalid aggregator ID")
+        (level, prefixes, wc) = agg_param
+        if len(public_share) != self.BITS:
+            raise ValueError("corrections words has incorrect length")
+        for p in prefixes:
+            if len(p) != level + 1:
+                raise ValueError("prefix with incorrect length")
+        pub = self.encode_public_share(public_share)
+        ins = self.test_vec_encode_input_share(input_share)
+        (ps, js, out, st) = self.prep_init_batch(verify_key, ctx, agg_id, agg_param, nonce, pub, ins)
+        if st[0] != 0:
+            raise ValueError("test point is a root of unity")
+        prep_share = self.decode_prep_share(wc, ps)
+        jr_seed = js[:32] if (wc and self.JOINT_RAND_LEN > 0) else None
+        return ((self.field.decode_vec(out), jr_seed), prep_share)
+
+    def prep_shares_to_prep(self, ctx, agg_param, prep_shares):
+        """poc/mastic.py:320-362"""
+        if len(prep_shares) != 2:
+            raise ValueError("unexpected number of prep shares")
+        (_level, _prefixes, wc) = agg_param
+        for ps in prep_shares:
+            if wc and ps[1] is None:
+                raise ValueError("expected FLP verifier shares")
+            if wc and self.JOINT_RAND_LEN > 0 and ps[2] is None:
+                raise ValueError("expected FLP joint randomness parts")
+        enc0 = self.test_vec_encode_prep_share(prep_shares[0] if wc else (prep_shares[0][0], None, None))
+        enc1 = self.test_vec_encode_prep_share(prep_shares[1] if wc else (prep_shares[1][0], None, None))
+        (msgs, valid) = self.decide_batch(ctx, agg_param, enc0, enc1)
+        if valid[0] == 0:
+            raise Exception("VIDPF verification failed")
+        if valid[0] == 2:
+            raise Exception("FLP verification failed")
+        if not wc or self.JOINT_RAND_LEN == 0:
+            return None
+        return msgs[:32]
+
+    def prep_next(self, _ctx, prep_state, prep_msg):
+        """poc/mastic.py:364-377"""
+        (truncated, jr_seed) = prep_state
+        if jr_seed is not None:
+            if prep_msg is None:
+                raise ValueError("expected joint rand confirmation")
+            if prep_msg != jr_seed:
+                raise Exception("joint rand confirmation failed")
+        return truncated
+
+    def agg_init(self, agg_param):
+        return self.field.zeros(len(agg_param[1]) * (1 + self.OUTPUT_LEN))
+
+    def agg_update(self, agg_param, agg_share, out_share):
+        return [a + b for (a, b) in zip(agg_share, out_share)]
+
+    def merge(self, agg_param, agg_shares):
+        agg = self.agg_init(agg_param)
+        for s in agg_shares:
+            agg = self.agg_update(agg_param, agg, s)
+        return agg
+
+    def unshard(self, agg_param, agg_shares, num_measurements):
+        """poc/mastic.py:399-411"""
+        agg = self.merge(agg_param, agg_shares)
+        k = 1 + self.OUTPUT_LEN
+        return [self.decode_result(agg[i + 1:i + k], agg[i].int()) for i in range(0, len(agg), k)]
+
+    # ----------------------------------------------------------- encodings
+    def encode_agg_param(self, agg_param) -> bytes:
+        """poc/mastic.py:413-435"""
+        (level, prefixes, do_weight_check) = agg_param
+        if not 0 <= level < 2 ** 16:
+            raise ValueError("level out of range")
+        if not 0 <= len(prefixes) < 2 ** 32:
+            raise ValueError("number of prefixes out of range")
+        out = level.to_bytes(2, "big") + len(prefixes).to_bytes(4, "big")
+        out += b"".join(_pack_path(p) for p in prefixes)
+        return out + bytes([int(bool(do_weight_check))])
+
+    def decode_agg_param(self, enc: bytes):
+        (level, count, wc) = self._agg_param_header(enc)
+        plen = (level + 1 + 7) // 8
+        if len(enc) != 6 + plen * count + 1:
+            raise ValueError("agg param has incorrect length")
+        prefixes = []
+        for i in range(count):
+            b = enc[6 + plen * i: 6 + plen * (i + 1)]
+            prefixes.append(tuple(bool((b[j // 8] >> (7 - j % 8)) & 1) for j in range(level + 1)))
+        return (level, tuple(prefixes), wc)
+
+    def encode_public_share(self, cws) -> bytes:
+        """Vidpf.encode_public_share (poc/vidpf.py:382-394)."""
+        if isinstance(cws, (bytes, bytearray)):
+            return bytes(cws)
+        out = _pack_bits_lsb(list(itertools.chain.from_iterable(cw[1] for cw in cws)))
+        out += b"".join(cw[0] for cw in cws)
+        out += b"".join(self.field.encode_vec(cw[2]) for cw in cws)
+        return out + b"".join(cw[3] for cw in cws)
+
+    def decode_public_share(self, data: bytes):
+        if len(data) != self.sizes.public_share_size:
+            raise ValueError("public share has incorrect length")
+        B = self.BITS
+        nb = (2 * B + 7) // 8
+        bits = [bool((data[i // 8] >> (i % 8)) & 1) for i in range(2 * B)]
+        pos = nb
+        seeds = [data[pos + 16 * i: pos + 16 * (i + 1)] for i in range(B)]
+        pos += 16 * B
+        wl = self.VALUE_LEN * self.field.ENCODED_SIZE
+        ws = [self.field.decode_vec(data[pos + wl * i: pos + wl * (i + 1)]) for i in range(B)]
+        pos += wl * B
+        proofs = [data[pos + 32 * i: pos + 32 * (i + 1)] for i in range(B)]
+        return [(seeds[i], [bits[2 * i], bits[2 * i + 1]], ws[i], proofs[i]) for i in range(B)]
+
+    test_vec_encode_public_share = encode_public_share
+
+    def test_vec_encode_input_share(self, input_share) -> bytes:
+        """poc/mastic.py:516-529"""
+        if isinstance(input_share, (bytes, bytearray)):
+            return bytes(input_share)
+        (key, proof_share, seed, peer) = input_share
+        out = key
+        if proof_share is not None:
+            out += self.field.encode_vec(proof_share)
+        if seed is not None:
+            out += seed
+        if peer is not None:
+            out += peer
+        return out
+
+    def decode_input_share(self, agg_id, data: bytes):
+        if len(data) != self.sizes.input_share_size[agg_id]:
+            raise ValueError("input share has incorrect length")
+        key, rest = data[:16], data[16:]
+        proof_share = seed = peer = None
+        if agg_id == 0:
+            k = self.PROOF_LEN * self.field.ENCODED_SIZE
+            proof_share, rest = self.field.decode_vec(rest[:k]), rest[k:]
+        if agg_id == 1 or self.JOINT_RAND_LEN > 0:
+            seed, rest = rest[:32], rest[32:]
+        if self.JOINT_RAND_LEN > 0:
+            peer = rest[:32]
+        return (key, proof_share, seed, peer)
+
+    def test_vec_encode_prep_share(self, prep_share) -> bytes:
+        """poc/mastic.py:543-552"""
+        (eval_proof, verifier, jr_part) = prep_share
+        out = eval_proof
+        if jr_part is not None:
+            out += jr_part
+        if verifier is not None:
+            out += self.field.encode_vec(verifier)
+        return out
+
+    def decode_prep_share(self, weight_check, data: bytes):
+        if len(data) != self.prep_share_size(weight_check):
+            raise ValueError("prep share has incorrect length")
+        ep, rest = data[:32], data[32:]
+        if not weight_check:
+            return (ep, None, None)
+        jp = None
+        if self.JOINT_RAND_LEN > 0:
+            jp, rest = rest[:32], rest[32:]
+        return (ep, self.field.decode_vec(rest), jp)
+
+    def test_vec_encode_prep_msg(self, msg) -> bytes:
+        return msg if msg is not None else b""
+
+    def test_vec_encode_agg_share(self, agg_share) -> bytes:
+        return self.field.encode_vec(agg_share) if len(agg_share) else b""
+
+
+class MasticCount(Mastic):
+    """poc/mastic.py:567-574"""
+    test_vec_name = "MasticCount"
+
+    def __init__(self, bits: int, device: int = 0):
+        super().__init__(bits, "Count", device=device)
+
+
+class MasticSum(Mastic):
+    """poc/mastic.py:577-584"""
+    test_vec_name = "MasticSum"
+
+    def __init__(self, bits: int, max_measurement: int, device: int = 0):
+        super().__init__(bits, "Sum", max_measurement=max_measurement, device=device)
+
+
+class MasticSumVec(Mastic):
+    """poc/mastic.py:587-594"""
+    test_vec_name = "MasticSumVec"
+
+    def __init__(self, bits: int, length: int, sum_vec_bits: int, chunk_length: int, device: int = 0):
+        super().__init__(bits, "SumVec", length=length, sum_vec_bits=sum_vec_bits,
+                         chunk_length=chunk_length, device=device)
+
+
+class MasticHistogram(Mastic):
+    """poc/mastic.py:597-604"""
+    test_vec_name = "MasticHistogram"
+
+    def __init__(self, bits: int, length: int, chunk_length: int, device: int = 0):
+        super().__init__(bits, "Histogram", length=length, chunk_length=chunk_length, device=device)
+
+
+class MasticMultihotCountVec(Mastic):
+    """poc/mastic.py:607-614"""
+    test_vec_name = "MasticMultihotCountVec"
+
+    def __init__(self, bits: int, length: int, max_weight: int, chunk_length: int, device: int = 0):
+        super().__init__(bits, "MultihotCountVec", length=length, max_measurement=max_weight,
+                         chunk_length=chunk_length, device=device)
+
+
+def from_test_vec(tv: dict, device: int = 0) -> Mastic:
+    bits = tv["vidpf_bits"]
+    if "max_measurement" in tv:
+        return MasticSum(bits, tv["max_measurement"], device=device)
+    if "max_weight" in tv:
+        return MasticMultihotCountVec(bits, tv["length"], tv["max_weight"], tv["chunk_length"], device=device)
+    if "bits" in tv:
+        return MasticSumVec(bits, tv["length"], tv["bits"], tv["chunk_length"], device=device)
+    if "length" in tv:
+        return MasticHistogram(bits, tv["length"], tv["chunk_length"], device=device)
+    return MasticCount(bits, device=device)

@@ -1,0 +1,170 @@
+/*
+ * mastic_hip.h — C ABI of the MI355X (gfx950) batched Mastic aggregator.
+ *
+ * Drop-in boundary for the reference's per-report Mastic API
+ * (poc/mastic.py, class Mastic :52-559, instantiations :567-614).  Every
+ * entry point is batch-first: it processes n reports that share one
+ * aggregation parameter, with caller-owned buffers holding the reference's
+ * wire encodings (test_vec/mastic format).  Plain pointers and sizes only.
+ *
+ *   reference (poc/)                         replaced by
+ *   ------------------------------------------------------------------
+ *   Mastic.__init__ / MasticCount.. :81-89,   mastic_ctx_create
+ *       :567-614
+ *   Mastic.shard :91-185                      mastic_shard_batch,
+ *   (Vidpf.gen vidpf.py:103-211)              mastic_reports_shard
+ *   Mastic.prep_init :205-318                 mastic_prep_init_batch,
+ *   (Vidpf.eval_with_siblings :213-261,       mastic_prep_init +
+ *    FlpBBCGGI19.query)                       mastic_prep_result
+ *   Mastic.prep_shares_to_prep :320-362       mastic_decide_batch
+ *   (FlpBBCGGI19.decide)
+ *   Mastic.agg_init/agg_update/merge          mastic_aggregate
+ *       :379-397
+ *   Mastic.encode_agg_param :413-435          (consumed as input, decoded here)
+ *
+ * Errors: 0 on success, a negative MASTIC_E* code otherwise (the reference's
+ * ValueError cases map to MASTIC_EINVAL; mastic_last_error() gives the text).
+ * Per-report verification outcomes are reported in status arrays instead of
+ * raising.  Calls block until their results are in the caller's buffers
+ * (mastic_prep_init is the exception: it only enqueues).  A ctx is
+ * thread-compatible, not thread-safe.  The library never frees caller memory.
+ *
+ * The product path has no CPU fallback: without a usable gfx950 device
+ * mastic_ctx_create fails with MASTIC_ENODEV.
+ */
+#ifndef MASTIC_HIP_H
+#define MASTIC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MASTIC_OK 0
+#define MASTIC_EINVAL (-22)
+#define MASTIC_ENOMEM (-12)
+#define MASTIC_ENODEV (-19)
+#define MASTIC_EHIP (-5)
+
+/* circuit ids = low byte of the reference's algorithm IDs (mastic.py:568-611) */
+#define MASTIC_COUNT 1            /* MasticCount(bits)                         */
+#define MASTIC_SUM 2              /* MasticSum(bits, max_measurement)          */
+#define MASTIC_SUMVEC 3           /* MasticSumVec(bits, length, bits, chunk)   */
+#define MASTIC_HISTOGRAM 4        /* MasticHistogram(bits, length, chunk)      */
+#define MASTIC_MULTIHOT 5         /* MasticMultihotCountVec(bits, len, max_w, chunk) */
+
+typedef struct mastic_params {
+    uint32_t circuit;
+    uint32_t bits;            /* VIDPF BITS */
+    uint32_t length;          /* SumVec / Histogram / MultihotCountVec length */
+    uint32_t sum_vec_bits;    /* SumVec bits */
+    uint64_t max_measurement; /* Sum max_measurement / MultihotCountVec max_weight */
+    uint32_t chunk_length;    /* SumVec / Histogram / MultihotCountVec chunk_length */
+    int32_t device;           /* HIP device ordinal */
+} mastic_params;
+
+typedef struct mastic_sizes {
+    uint32_t field_bytes;       /* ENCODED_SIZE: 8 (Field64) or 16 (Field128) */
+    uint32_t value_len;         /* VIDPF VALUE_LEN = 1 + MEAS_LEN */
+    uint32_t meas_len;
+    uint32_t output_len;
+    uint32_t proof_len;
+    uint32_t verifier_len;
+    uint32_t joint_rand_len;
+    uint32_t query_rand_len;
+    uint32_t prove_rand_len;
+    uint32_t rand_size;         /* Mastic.RAND_SIZE */
+    uint32_t public_share_size;
+    uint32_t input_share_size[2];
+    uint32_t prep_share_size[2]; /* [0] without, [1] with the weight check */
+    uint32_t algorithm_id;
+} mastic_sizes;
+
+typedef struct mastic_ctx mastic_ctx;
+typedef struct mastic_reports mastic_reports;
+
+int mastic_ctx_create(const mastic_params* params, mastic_ctx** out);
+void mastic_ctx_destroy(mastic_ctx* ctx);
+const char* mastic_last_error(const mastic_ctx* ctx);
+int mastic_get_sizes(const mastic_ctx* ctx, mastic_sizes* out);
+/* Device-memory budget (bytes) for one prep_init batch's work buffers; 0 = default. */
+int mastic_set_memory_budget(mastic_ctx* ctx, uint64_t bytes);
+
+/* ---- reports resident in HBM (wire encodings, report-major) ---------- */
+int mastic_reports_create(mastic_ctx* ctx, size_t n, mastic_reports** out);
+void mastic_reports_destroy(mastic_reports* rep);
+size_t mastic_reports_count(const mastic_reports* rep);
+/* nonces n*16, public_shares n*public_share_size, input_shares{0,1}
+ * n*input_share_size[agg]; either input-share pointer may be NULL. */
+int mastic_reports_upload(mastic_reports* rep, const uint8_t* nonces, const uint8_t* public_shares,
+                          const uint8_t* input_shares0, const uint8_t* input_shares1);
+int mastic_reports_download(mastic_reports* rep, uint8_t* nonces, uint8_t* public_shares,
+                            uint8_t* input_shares0, uint8_t* input_shares1);
+/* Client shard on the GPU (Mastic.shard).  alphas n*ceil(bits/8) MSB-first,
+ * betas n*meas_len*field_bytes = the FLP-encoded measurement (Valid.encode),
+ * nonces n*16, rands n*rand_size. */
+int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* alphas,
+                         const uint8_t* betas, const uint8_t* nonces, const uint8_t* rands);
+
+/* ---- aggregator preparation ----------------------------------------- */
+/* Enqueue prep_init for every report of `rep` as aggregator agg_id.
+ * enc_agg_param is Mastic.encode_agg_param's output.  Results stay in HBM
+ * (one result slot per agg_id) until read or aggregated. */
+int mastic_prep_init(mastic_ctx* ctx, mastic_reports* rep, const uint8_t verify_key[32], const uint8_t* app_ctx,
+                     size_t ctx_len, int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len);
+/* Copy results of the last mastic_prep_init for agg_id (blocks).  Any output
+ * may be NULL.  prep_shares n*prep_share_size[weight_check] (wire encoding,
+ * mastic.py:543-552); jr_seeds n*32 (zero when not applicable);
+ * out_shares n*len(prefixes)*(1+output_len)*field_bytes (truncated output
+ * shares = prep_state[0], encode_vec); status n (0 = ok, <0 = query abort). */
+int mastic_prep_result(mastic_ctx* ctx, int agg_id, uint8_t* prep_shares, uint8_t* jr_seeds, uint8_t* out_shares,
+                       int32_t* status);
+/* Fold the out shares of the last prep_init for agg_id over the reports whose
+ * valid[i] != 0 (valid == NULL: all) into agg_share
+ * (len(prefixes)*(1+output_len)*field_bytes, encode_vec). */
+int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t* agg_share);
+/* Wait for all enqueued work of the ctx. */
+int mastic_synchronize(mastic_ctx* ctx);
+
+/* One-shot host-buffer form of upload + prep_init + prep_result. */
+int mastic_prep_init_batch(mastic_ctx* ctx, const uint8_t verify_key[32], const uint8_t* app_ctx, size_t ctx_len,
+                           int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len, size_t n,
+                           const uint8_t* nonces, const uint8_t* public_shares, const uint8_t* input_shares,
+                           uint8_t* prep_shares_out, uint8_t* jr_seeds_out, uint8_t* out_shares_out,
+                           int32_t* status_out);
+
+/* prep_shares_to_prep for n report pairs.  prep_msgs_out n*32 (joint-rand
+ * confirmation seed; untouched when the circuit has no joint randomness) may
+ * be NULL.  valid_out[i]: MASTIC_DECIDE_OK when both checks pass (eval proofs
+ * equal and, with the weight check, the FLP decides true);
+ * MASTIC_DECIDE_VIDPF_FAIL / MASTIC_DECIDE_FLP_FAIL mirror the reference's
+ * 'VIDPF verification failed' / 'FLP verification failed' exceptions. */
+#define MASTIC_DECIDE_VIDPF_FAIL 0
+#define MASTIC_DECIDE_OK 1
+#define MASTIC_DECIDE_FLP_FAIL 2
+int mastic_decide_batch(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* enc_agg_param,
+                        size_t agg_param_len, size_t n, const uint8_t* prep_shares0, const uint8_t* prep_shares1,
+                        uint8_t* prep_msgs_out, uint8_t* valid_out);
+
+/* One-shot client shard of n reports into host buffers. */
+int mastic_shard_batch(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_len, size_t n, const uint8_t* alphas,
+                       const uint8_t* betas, const uint8_t* nonces, const uint8_t* rands, uint8_t* public_shares_out,
+                       uint8_t* input_shares0_out, uint8_t* input_shares1_out);
+
+/* ---- measurement hooks (bench) --------------------------------------- */
+/* Device time (ms) of the VIDPF level-eval kernels and of the binder-absorb
+ * kernels during the last prep_init, measured with HIP events on the ctx's
+ * stream; also their launch counts. */
+int mastic_last_timing(mastic_ctx* ctx, double* eval_ms, int* eval_launches, double* absorb_ms,
+                       int* absorb_launches, double* total_ms);
+/* Tree statistics of an encoded agg param: nodes evaluated per report,
+ * interior nodes, max nodes on one level. */
+int mastic_tree_stats(mastic_ctx* ctx, const uint8_t* enc_agg_param, size_t agg_param_len, uint64_t* nodes,
+                      uint64_t* interior, uint64_t* max_level_nodes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

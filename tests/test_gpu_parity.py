@@ -1,0 +1,344 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle and the
+reference's golden vectors.  Bit-exact everywhere: all of this is integer,
+byte and GF(p) arithmetic.
+
+Sizes: the golden vectors; random reports for every circuit at sizes the
+oracle finishes in seconds; the C2 bench shape (BITS 32, Sum 255) with a
+large prefix set checked through size-independent properties plus one report
+replayed in the oracle.
+"""
+import json
+import os
+import random
+
+import pytest
+
+from conftest import golden_files
+
+pytestmark = pytest.mark.gpu
+
+CTX = b"some application"
+
+
+@pytest.fixture(scope="module")
+def mastic_amd():
+    import mastic_amd
+    from mastic_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libmastic_hip.so missing: build() was not run")
+    try:
+        mastic_amd.MasticCount(2)
+    except _lib.MasticError as e:
+        if e.code == -19:
+            pytest.skip("no gfx950 device")
+        raise
+    return mastic_amd
+
+
+def _oracle_for(m):
+    from oracle import mastic as om
+    c = m.circuit
+    if c == "Count":
+        return om.MasticCount(m.BITS)
+    if c == "Sum":
+        return om.MasticSum(m.BITS, m.max_measurement)
+    if c == "SumVec":
+        return om.MasticSumVec(m.BITS, m.length, m.sum_vec_bits, m.chunk_length)
+    if c == "Histogram":
+        return om.MasticHistogram(m.BITS, m.length, m.chunk_length)
+    return om.MasticMultihotCountVec(m.BITS, m.length, m.max_measurement, m.chunk_length)
+
+
+# ------------------------------------------------------------ golden vectors
+@pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
+def test_golden_vector_on_gpu(mastic_amd, path):
+    tv = json.load(open(path))
+    m = mastic_amd.from_test_vec(tv)
+    ctx = bytes.fromhex(tv["ctx"])
+    vk = bytes.fromhex(tv["verify_key"])
+    ap = m.decode_agg_param(bytes.fromhex(tv["agg_param"]))
+    reps = tv["prep"]
+    # client shard on the GPU
+    alphas = [tuple(r["measurement"][0]) for r in reps]
+    weights = [r["measurement"][1] for r in reps]
+    nonces = b"".join(bytes.fromhex(r["nonce"]) for r in reps)
+    rands = b"".join(bytes.fromhex(r["rand"]) for r in reps)
+    (pub, in0, in1) = m.shard_batch(ctx, alphas, weights, nonces, rands)
+    assert pub == b"".join(bytes.fromhex(r["public_share"]) for r in reps)
+    assert in0 == b"".join(bytes.fromhex(r["input_shares"][0]) for r in reps)
+    assert in1 == b"".join(bytes.fromhex(r["input_shares"][1]) for r in reps)
+    # prep_init, both aggregators
+    shares = []
+    for a in range(2):
+        ins = in0 if a == 0 else in1
+        (ps, js, out, st) = m.prep_init_batch(vk, ctx, a, ap, nonces, pub, ins)
+        assert list(st) == [0] * len(reps)
+        assert ps == b"".join(bytes.fromhex(r["prep_shares"][0][a]) for r in reps)
+        want_out = b"".join(b"".join(bytes.fromhex(x) for x in r["out_shares"][a]) for r in reps)
+        assert out == want_out
+        shares.append(ps)
+        agg = m.aggregate_device(a, ap)
+        assert m.test_vec_encode_agg_share(agg).hex() == tv["agg_shares"][a]
+    (msgs, valid) = m.decide_batch(ctx, ap, shares[0], shares[1])
+    assert list(valid) == [1] * len(reps)
+    for (i, r) in enumerate(reps):
+        if r["prep_messages"][0]:
+            assert msgs[32 * i:32 * (i + 1)].hex() == r["prep_messages"][0]
+    aggs = [m.aggregate_device(a, ap) for a in range(2)]
+    assert m.unshard(ap, aggs, len(reps)) == tv["agg_result"]
+
+
+def test_reference_shaped_api_one_report(mastic_amd):
+    """The per-report methods mirror poc/mastic.py and agree with the oracle."""
+    tv = json.load(open(golden_files()[4]))  # MasticHistogram_0
+    m = mastic_amd.from_test_vec(tv)
+    o = _oracle_for(m)
+    ctx = bytes.fromhex(tv["ctx"])
+    vk = bytes.fromhex(tv["verify_key"])
+    ap = m.decode_agg_param(bytes.fromhex(tv["agg_param"]))
+    rep = tv["prep"][0]
+    meas = (tuple(rep["measurement"][0]), rep["measurement"][1])
+    nonce = bytes.fromhex(rep["nonce"])
+    rand = bytes.fromhex(rep["rand"])
+    (cws, ins) = m.shard(ctx, meas, nonce, rand)
+    (ocws, oins) = o.shard(ctx, meas, nonce, rand)
+    assert m.encode_public_share(cws) == o.test_vec_encode_public_share(ocws)
+    states, shares = [], []
+    for a in range(2):
+        (st, sh) = m.prep_init(vk, ctx, a, ap, nonce, cws, ins[a])
+        (ost, osh) = o.prep_init(vk, ctx, a, ap, nonce, ocws, oins[a])
+        assert m.test_vec_encode_prep_share(sh) == o.test_vec_encode_prep_share(osh)
+        assert [x.int() for x in st[0]] == [x.int() for x in ost[0]]
+        assert st[1] == ost[1]
+        states.append(st)
+        shares.append(sh)
+    msg = m.prep_shares_to_prep(ctx, ap, shares)
+    assert msg == o.prep_shares_to_prep(ctx, ap, [o.decode_prep_share(True, m.test_vec_encode_prep_share(s))
+                                                  for s in shares])
+    outs = [m.prep_next(ctx, states[a], msg) for a in range(2)]
+    assert m.unshard(ap, outs, 1) == o.unshard(ap, [[o.field(x.int()) for x in y] for y in outs], 1)
+
+
+# ------------------------------------------------------------ random parity
+def _random_reports(m, rng, n):
+    alphas, weights = [], []
+    for _ in range(n):
+        alphas.append(tuple(bool(rng.getrandbits(1)) for _ in range(m.BITS)))
+        c = m.circuit
+        if c == "Count":
+            weights.append(rng.randrange(2))
+        elif c == "Sum":
+            weights.append(rng.randrange(m.max_measurement + 1))
+        elif c == "SumVec":
+            weights.append([rng.randrange(2 ** m.sum_vec_bits) for _ in range(m.length)])
+        elif c == "Histogram":
+            weights.append(rng.randrange(m.length))
+        else:
+            k = rng.randrange(m.max_measurement + 1)
+            idx = set(rng.sample(range(m.length), k))
+            weights.append([i in idx for i in range(m.length)])
+    nonces = bytes(rng.getrandbits(8) for _ in range(16 * n))
+    rands = bytes(rng.getrandbits(8) for _ in range(m.RAND_SIZE * n))
+    return alphas, weights, nonces, rands
+
+
+def _random_agg_param(m, rng, alphas, level, nprefix, weight_check):
+    cand = set(tuple(a[:level + 1]) for a in alphas)
+    while len(cand) < nprefix and len(cand) < 2 ** (level + 1):
+        cand.add(tuple(bool(rng.getrandbits(1)) for _ in range(level + 1)))
+    pre = list(cand)[:nprefix]
+    rng.shuffle(pre)
+    return (level, tuple(pre), weight_check)
+
+
+def _check_against_oracle(m, o, ctx, vk, ap, alphas, weights, nonces, rands, check_shard=True):
+    n = len(alphas)
+    (pub, in0, in1) = m.shard_batch(ctx, alphas, weights, nonces, rands)
+    ps_sz, is_sz = m.public_share_size(), [m.input_share_size(0), m.input_share_size(1)]
+    gpu = {}
+    for a in range(2):
+        gpu[a] = m.prep_init_batch(vk, ctx, a, ap, nonces, pub, in0 if a == 0 else in1)
+        assert list(gpu[a][3]) == [0] * n
+    oshares = [[], []]
+    for i in range(n):
+        nonce = nonces[16 * i:16 * (i + 1)]
+        meas = (alphas[i], weights[i])
+        if check_shard:
+            (ocws, oins) = o.shard(ctx, meas, nonce, rands[m.RAND_SIZE * i:m.RAND_SIZE * (i + 1)])
+            assert o.test_vec_encode_public_share(ocws) == pub[ps_sz * i:ps_sz * (i + 1)]
+            assert o.test_vec_encode_input_share(oins[0]) == in0[is_sz[0] * i:is_sz[0] * (i + 1)]
+            assert o.test_vec_encode_input_share(oins[1]) == in1[is_sz[1] * i:is_sz[1] * (i + 1)]
+        else:
+            ocws = o.vidpf.decode_public_share(pub[ps_sz * i:ps_sz * (i + 1)])
+            oins = [o.decode_input_share(0, in0[is_sz[0] * i:is_sz[0] * (i + 1)]),
+                    o.decode_input_share(1, in1[is_sz[1] * i:is_sz[1] * (i + 1)])]
+        for a in range(2):
+            (ost, osh) = o.prep_init(vk, ctx, a, ap, nonce, ocws, oins[a])
+            enc = o.test_vec_encode_prep_share(osh)
+            (ps, js, out, _st) = gpu[a]
+            assert ps[len(enc) * i:len(enc) * (i + 1)] == enc, "prep share %d agg %d" % (i, a)
+            ow = len(out) // n
+            assert out[ow * i:ow * (i + 1)] == o.field.encode_vec(ost[0]), "out share %d agg %d" % (i, a)
+            if ost[1] is not None:
+                assert js[32 * i:32 * (i + 1)] == ost[1]
+            oshares[a].append(enc)
+    (msgs, valid) = m.decide_batch(ctx, ap, gpu[0][0], gpu[1][0])
+    assert list(valid) == [1] * n
+    for i in range(n):
+        omsg = o.prep_shares_to_prep(ctx, ap, [o.decode_prep_share(ap[2], oshares[a][i]) for a in range(2)])
+        if omsg is not None:
+            assert msgs[32 * i:32 * (i + 1)] == omsg
+    return gpu
+
+
+CASES = [
+    ("Count", dict(bits=6)),
+    ("Sum", dict(bits=5, max_measurement=13)),
+    ("SumVec", dict(bits=4, length=5, sum_vec_bits=3, chunk_length=4)),
+    ("Histogram", dict(bits=5, length=7, chunk_length=3)),
+    ("MultihotCountVec", dict(bits=4, length=6, max_measurement=3, chunk_length=2)),
+]
+
+
+@pytest.mark.parametrize("circuit,kw", CASES, ids=[c for (c, _) in CASES])
+def test_random_reports_match_oracle(mastic_amd, circuit, kw):
+    rng = random.Random(sum(map(ord, circuit)))
+    kw = dict(kw)
+    bits = kw.pop("bits")
+    m = mastic_amd.Mastic(bits, circuit, **kw)
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 5)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    for (level, nprefix, wc) in [(0, 2, True), (bits - 1, 6, True), (bits // 2, 3, False)]:
+        ap = _random_agg_param(m, rng, alphas, level, nprefix, wc)
+        _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=(level == 0))
+
+
+def test_long_context_string(mastic_amd):
+    """A ctx longer than one TurboSHAKE block moves every sponge prefix over a
+    block boundary (prefix states with full blocks absorbed)."""
+    rng = random.Random(7)
+    m = mastic_amd.MasticSum(4, 5)
+    o = _oracle_for(m)
+    ctx = bytes(rng.getrandbits(8) for _ in range(301))
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 3)
+    vk = bytes(range(32))
+    ap = _random_agg_param(m, rng, alphas, 3, 4, True)
+    _check_against_oracle(m, o, ctx, vk, ap, alphas, weights, nonces, rands)
+
+
+def test_empty_ctx_and_single_prefix(mastic_amd):
+    rng = random.Random(8)
+    m = mastic_amd.MasticCount(3)
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 2)
+    ap = (2, (alphas[0],), True)
+    _check_against_oracle(m, o, b"", bytes(32), ap, alphas, weights, nonces, rands)
+
+
+def test_chunked_batches_equal_unchunked(mastic_amd):
+    """Reports processed in several HBM-budget chunks give identical results."""
+    rng = random.Random(9)
+    m = mastic_amd.MasticCount(8)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 150)
+    (pub, in0, _in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    ap = _random_agg_param(m, rng, alphas, 7, 20, True)
+    vk = bytes(32)
+    full = m.prep_init_batch(vk, CTX, 0, ap, nonces, pub, in0)
+    agg_full = m.aggregate_device(0, ap)
+    from mastic_amd import _lib
+    try:
+        # ~5 KB of work planes per report here: a 400 KB budget -> 64-report chunks
+        _lib.lib().mastic_set_memory_budget(m._ctx, 400_000)
+        m2 = m.prep_init_batch(vk, CTX, 0, ap, nonces, pub, in0)
+    finally:
+        _lib.lib().mastic_set_memory_budget(m._ctx, 0)
+    assert m2[0] == full[0] and m2[2] == full[2]
+    assert m.aggregate_device(0, ap) == agg_full
+
+
+def test_malformed_payload_correction_word_detected(mastic_amd):
+    """poc/tests/test_mastic.py:126-175: tweak a payload CW -> eval proofs differ."""
+    rng = random.Random(10)
+    m = mastic_amd.MasticCount(5)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 4)
+    alphas[0] = (True,) * 5
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    bad_level = 2
+    cws = m.decode_public_share(pub[:m.public_share_size()])
+    (s, c, w, p) = cws[bad_level]
+    w = list(w)
+    w[1] = w[1] + m.field(1)
+    cws[bad_level] = (s, c, w, p)
+    pub = m.encode_public_share(cws) + pub[m.public_share_size():]
+    vk = bytes(32)
+    for level in range(5):
+        ap = (level, ((True,) * (level + 1),), False)
+        sh = [m.prep_init_batch(vk, CTX, a, ap, nonces, pub, in0 if a == 0 else in1)[0] for a in range(2)]
+        (_msgs, valid) = m.decide_batch(CTX, ap, sh[0], sh[1])
+        assert valid[0] == (1 if level < bad_level else 0)
+        assert list(valid[1:]) == [1, 1, 1]
+
+
+def test_invalid_weight_rejected_by_flp(mastic_amd):
+    """A client that encodes an out-of-range weight fails the FLP decide."""
+    rng = random.Random(11)
+    m = mastic_amd.MasticSum(3, 3)  # b = 2 bits
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 2)
+    F = m.field
+    bad = [F(1), F(1), F(0), F(1)]   # 3 with inconsistent offset bits
+    ok = m.encode_measurement(2)
+    ab = bytes([(sum(int(b) << (7 - i) for (i, b) in enumerate(a[:8]))) & 0xff for a in alphas])
+    betas = F.encode_vec(bad) + F.encode_vec(ok)
+    (pub, in0, in1) = m.shard_encoded(CTX, 2, ab, betas, nonces, rands)
+    ap = (0, ((False,), (True,)), True)
+    sh = [m.prep_init_batch(bytes(32), CTX, a, ap, nonces, pub, in0 if a == 0 else in1)[0] for a in range(2)]
+    (_msgs, valid) = m.decide_batch(CTX, ap, sh[0], sh[1])
+    assert list(valid) == [2, 1]
+
+
+def test_errors_mirror_reference(mastic_amd):
+    m = mastic_amd.MasticCount(4)
+    with pytest.raises(ValueError):
+        m.tree_stats(m.encode_agg_param((4, ((True,) * 5,), True)))          # level too deep
+    with pytest.raises(ValueError):
+        m.tree_stats(m.encode_agg_param((1, ((True, False), (True, False)), True)))  # non-unique
+
+
+# ------------------------------------------------------------ full size
+def test_c2_shape_properties_and_oracle_sample(mastic_amd):
+    """BASELINE config C2 shape: Mastic(32, Sum 255), level 31, 2000 candidate
+    prefixes (the bench uses 10k).  Size-independent checks over 128 reports:
+    both aggregators' eval proofs agree, FLP decides every report valid, and
+    the aggregate equals the plaintext functionality (talks/func.py:49-80).
+    One report is replayed in the CPU oracle at full tree size."""
+    rng = random.Random(12)
+    m = mastic_amd.MasticSum(32, 255)
+    attrs = [tuple(bool(rng.getrandbits(1)) for _ in range(32)) for _ in range(2000)]
+    attrs = list(dict.fromkeys(attrs))
+    n = 128
+    alphas = [attrs[rng.randrange(len(attrs))] for _ in range(n)]
+    weights = [rng.randrange(256) for _ in range(n)]
+    nonces = bytes(rng.getrandbits(8) for _ in range(16 * n))
+    rands = bytes(rng.getrandbits(8) for _ in range(m.RAND_SIZE * n))
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    ap = (31, tuple(sorted(attrs)), True)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    res = [m.prep_init_batch(vk, CTX, a, ap, nonces, pub, in0 if a == 0 else in1, want_out_shares=False)
+           for a in range(2)]
+    (_msgs, valid) = m.decide_batch(CTX, ap, res[0][0], res[1][0])
+    assert list(valid) == [1] * n
+    aggs = [m.aggregate_device(a, ap) for a in range(2)]
+    result = m.unshard(ap, aggs, n)
+    want = {}
+    for (a, w) in zip(alphas, weights):
+        want[a] = want.get(a, 0) + w
+    assert result == [want.get(p, 0) for p in ap[1]]
+    # one report through the oracle at full size
+    o = _oracle_for(m)
+    i = 0
+    cws = o.vidpf.decode_public_share(pub[:m.public_share_size()])
+    isd = o.decode_input_share(1, in1[:m.input_share_size(1)])
+    (_st, sh) = o.prep_init(vk, CTX, 1, ap, nonces[:16], cws, isd)
+    enc = o.test_vec_encode_prep_share(sh)
+    assert res[1][0][:len(enc)] == enc
