@@ -1,0 +1,260 @@
+"""Benchmark: VIDPF report x prefix evaluations/sec for Mastic prep_init +
+aggregate on MI355X (BASELINE.json metric), config C2:
+Mastic(BITS=32, Sum max=255), 10k candidate prefixes at level 31, weight
+check on, leader side (agg_id 0).
+
+A step = one pass of the hot path over one batch of reports resident in HBM:
+prep_init (VIDPF level walk, binder sponges, eval proof, FLP query) + the
+aggregate fold of all out shares; with N > 1 ranks also the RCCL all-gather
+of the per-rank agg shares and the on-GPU mod-p merge.  Reports are sharded
+over ranks (independent units, weak scaling).
+
+    python bench.py [--gpus N --steps K --warmup W --reports R --prefixes P]
+    (N > 1: launched by torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "draft-mouris-cfrg-mastic_amd"))
+
+METRIC = "VIDPF report x prefix evals/sec at 1/2/4/8 GPUs; % of int-VALU peak"
+# Fixed op-cost convention: int32 ops
+AES_BLOCK_OPS = 340
+KECCAK_OPS = 3720
+F64_ADD_OPS = 4
+# int32 VALU peak: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reports", type=int, default=4096, help="reports per rank per step")
+    ap.add_argument("--prefixes", type=int, default=10000)
+    ap.add_argument("--agg-id", type=int, default=0)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU baseline leg")
+    ap.add_argument("--cpu-procs", type=int, default=16)
+    return ap.parse_args()
+
+
+def synth(rank, n_reports, n_prefixes, seed=0x4D41 + 2):
+    """Synthetic C2 inputs: 10k random 32-bit attributes,
+    alphas uniform over them, weights uniform 0..255, distinct random nonces."""
+    rng = np.random.default_rng(seed)
+    attrs = np.unique(rng.integers(0, 2 ** 32, size=n_prefixes, dtype=np.uint64).astype(np.uint32))
+    while len(attrs) < n_prefixes:
+        attrs = np.unique(np.concatenate([attrs, rng.integers(0, 2 ** 32, size=n_prefixes - len(attrs),
+                                                              dtype=np.uint64).astype(np.uint32)]))
+    attrs = np.sort(attrs)
+    rrng = np.random.default_rng(seed * 1000003 + rank)
+    alphas = attrs[rrng.integers(0, len(attrs), size=n_reports)]
+    weights = rrng.integers(0, 256, size=n_reports)
+    nonces = rrng.integers(0, 256, size=16 * n_reports, dtype=np.uint8).tobytes()
+    return attrs, alphas, weights, nonces, rrng
+
+
+def encode_inputs(m, alphas, weights, rrng):
+    n = len(alphas)
+    alpha_b = alphas.astype(">u4").tobytes()  # MSB-first 32-bit paths
+    bits = ((weights[:, None] >> np.arange(8)) & 1).astype("<u8")  # Sum(255): b = 8, offset 0
+    betas = np.concatenate([bits, bits], axis=1).tobytes()
+    rands = rrng.integers(0, 256, size=m.RAND_SIZE * n, dtype=np.uint8).tobytes()
+    return alpha_b, betas, rands
+
+
+def agg_param_bytes(attrs):
+    return (31).to_bytes(2, "big") + len(attrs).to_bytes(4, "big") + attrs.astype(">u4").tobytes() + b"\x01"
+
+
+# ---------------------------------------------------------------- CPU baseline
+def _cpu_worker(job):
+    (enc_ap, nonce, pub, ins, vk, ctx, agg_id) = job
+    sys.path.insert(0, ROOT)
+    from oracle.mastic import MasticSum
+    o = MasticSum(32, 255)
+    ap = o.decode_agg_param(enc_ap)
+    cws = o.vidpf.decode_public_share(pub)
+    isd = o.decode_input_share(agg_id, ins)
+    t = time.perf_counter()
+    (_st, sh) = o.prep_init(vk, ctx, agg_id, ap, nonce, cws, isd)
+    dt = time.perf_counter() - t
+    return (dt, o.test_vec_encode_prep_share(sh))
+
+
+def cpu_baseline(jobs, procs):
+    import multiprocessing as mp
+    t = time.perf_counter()
+    if procs == 1:
+        res = [_cpu_worker(j) for j in jobs]
+    else:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t
+    return wall, res
+
+
+# ---------------------------------------------------------------- main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from mastic_amd import MasticSum, _lib
+    import ctypes
+
+    m = MasticSum(32, 255, device=local)
+    ctx = b"mastic-mi355x-bench"
+    attrs, alphas, weights, nonces, rrng = synth(rank, args.reports, args.prefixes)
+    alpha_b, betas, rands = encode_inputs(m, alphas, weights, rrng)
+    vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
+    enc_ap = agg_param_bytes(attrs)
+    reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
+    (nodes, interior, _maxl) = m.tree_stats(enc_ap)
+    n_elems = len(attrs) * (1 + m.OUTPUT_LEN)
+
+    def step():
+        m.prep_init_device(reps, vk, ctx, args.agg_id, enc_ap)
+        agg = m.aggregate_device(args.agg_id, enc_ap)
+        if world > 1:
+            local_share = torch.frombuffer(bytearray(m.field.encode_vec(agg)), dtype=torch.uint8).cuda()
+            gathered = torch.empty(world * local_share.numel(), dtype=torch.uint8, device="cuda")
+            dist.all_gather_into_tensor(gathered, local_share)
+            merged = torch.empty_like(local_share)
+            torch.cuda.synchronize()
+            rc = _lib.lib().mastic_fold_shares(m._ctx, ctypes.c_void_p(gathered.data_ptr()), world, n_elems,
+                                               ctypes.c_void_p(merged.data_ptr()))
+            assert rc == 0, rc
+        return agg
+
+    for _ in range(args.warmup):
+        step()
+    m.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eval_ms = absorb_ms = total_ms = 0.0
+    eval_n = absorb_n = 0
+    for _ in range(args.steps):
+        step()
+        (e, ne, a, na, t) = m.last_timing()
+        eval_ms += e
+        eval_n += ne
+        absorb_ms += a
+        absorb_n += na
+        total_ms += t
+    m.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    units = args.reports * len(attrs) * args.steps * world
+    value = units / dt
+    # roofline of the dominant kernel (k_eval_level): algorithmic int32 ops
+    aes_per_node = 1 + (16 + m.VALUE_LEN * m.field.ENCODED_SIZE + 15) // 16
+    ops_per_node = aes_per_node * AES_BLOCK_OPS + KECCAK_OPS + 2 * m.VALUE_LEN * F64_ADD_OPS
+    eval_ops = nodes * args.reports * args.steps * ops_per_node
+    achieved = eval_ops / (eval_ms / 1e3) / 1e12 if eval_ms > 0 else 0.0
+    # binder sponges: one-hot 32 B/node, payload VL*ENC B/interior node
+    absorb_perms = (32 * nodes + m.VALUE_LEN * m.field.ENCODED_SIZE * interior) / 168.0
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "report*prefix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C2: Mastic(BITS=32, Sum max=255) prep_init+aggregate, %d reports x %d prefixes per "
+                        "rank per step, level 31, weight check, agg_id %d" % (args.reports, len(attrs), args.agg_id),
+            "reports_per_step": args.reports * world,
+            "prefixes": len(attrs),
+            "nodes_per_report": nodes,
+            "field": "Field64",
+            "parallelism": "reports sharded %d-way" % world,
+        },
+        "roofline": {
+            "kernel": "k_eval_level<F64>",
+            "bound": "valu",
+            "achieved": achieved,
+            "peak": VALU_PEAK_TOPS,
+            "unit": "Tops/s (int32)",
+            "frac": achieved / VALU_PEAK_TOPS,
+            "traffic": None,
+            "launches": eval_n,
+            "avg_launch_ms": eval_ms / max(eval_n, 1),
+            "ops_per_node": ops_per_node,
+        },
+        "breakdown_ms_per_step": {
+            "eval_levels": eval_ms / args.steps,
+            "absorb_levels": absorb_ms / args.steps,
+            "prep_init_total": total_ms / args.steps,
+            "absorb_keccak_perms_per_report": absorb_perms,
+        },
+    }
+    traffic_file = os.path.join(ROOT, "profiles", "eval_traffic.json")
+    if os.path.exists(traffic_file):
+        tr = json.load(open(traffic_file))
+        if tr.get("prefixes") == len(attrs) and tr.get("reports") == args.reports:
+            out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        procs = min(args.cpu_procs, os.cpu_count() or 1)
+        (rn, pub, in0, in1) = reps.download()
+        ps = m.sizes.public_share_size
+        isz = m.sizes.input_share_size[args.agg_id]
+        ins = in0 if args.agg_id == 0 else in1
+        jobs = [(enc_ap, rn[16 * i:16 * (i + 1)], pub[ps * i:ps * (i + 1)], ins[isz * i:isz * (i + 1)], vk, ctx,
+                 args.agg_id) for i in range(procs)]
+        wall, res = cpu_baseline(jobs, procs)
+        # the same reports through the GPU path: parity of the timed workload
+        (gps, _js, _out, _st) = m.prep_init_batch(vk, ctx, args.agg_id, enc_ap, rn[:16 * procs],
+                                                  pub[:ps * procs], ins[:isz * procs], want_out_shares=False)
+        psz = m.prep_share_size(True)
+        parity = all(gps[psz * i:psz * (i + 1)] == res[i][1] for i in range(procs))
+        per_report = sum(r[0] for r in res) / len(res)
+        out["cpu_baseline"] = {
+            "value": procs * len(attrs) / wall,
+            "unit": "report*prefix/s",
+            "cores": procs,
+            "kind": "port",
+            "sample": "%d reports x %d prefixes, one per process (multiprocessing spawn pool of %d); "
+                      "poc-faithful Python oracle with C AES/TurboSHAKE; %.1f s per report per core "
+                      "(single-core %.0f report*prefix/s); GPU/CPU prep shares bit-identical: %s"
+                      % (procs, len(attrs), procs, per_report, len(attrs) / per_report, parity),
+        }
+        out["cpu_parity"] = parity
+    if rank == 0:
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -589,6 +589,21 @@ __global__ __launch_bounds__(256) void k_fold(const uint32_t* out, int n, int st
     }
 }
 
+// out[e] = sum_s in[s][e] (mod p): merges the agg shares gathered from the
+// ranks of a multi-GPU job (RCCL's sum is not GF(p) addition).
+template <class F>
+__global__ __launch_bounds__(256) void k_fold_shares(const uint32_t* in, int n_shares, int n_elems, uint32_t* out) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= n_elems) return;
+    typename F::E acc = F::zero();
+    for (int s = 0; s < n_shares; s++) {
+        uint32_t w[F::W32];
+        for (int i = 0; i < F::W32; i++) w[i] = in[((size_t)s * n_elems + e) * F::W32 + i];
+        acc = F::add(acc, F::from_words(w));
+    }
+    for (int i = 0; i < F::W32; i++) out[(size_t)e * F::W32 + i] = F::word(acc, i);
+}
+
 // ------------------------------------------------------------- decide
 // prep_shares_to_prep (mastic.py:320-362) for a batch of report pairs.
 // prep share wire: eval_proof || [jr_part] || [verifier]  (mastic.py:543-552)

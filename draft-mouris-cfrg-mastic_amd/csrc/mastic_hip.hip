@@ -673,6 +673,23 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     return 0;
 }
 
+extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t n_shares, size_t n_elems,
+                                  void* dev_out) {
+    if (!c || (!dev_shares && n_shares) || !dev_out) return MASTIC_EINVAL;
+    if (n_elems == 0) return 0;
+    HIPCHK(c, hipDeviceSynchronize());  // the shares may come from another stream (RCCL)
+    const dim3 grid((unsigned)((n_elems + 255) / 256));
+    if (c->p.field == 64)
+        hipLaunchKernelGGL(k_fold_shares<F64>, grid, dim3(256), 0, c->stream, (const uint32_t*)dev_shares,
+                           (int)n_shares, (int)n_elems, (uint32_t*)dev_out);
+    else
+        hipLaunchKernelGGL(k_fold_shares<F128>, grid, dim3(256), 0, c->stream, (const uint32_t*)dev_shares,
+                           (int)n_shares, (int)n_elems, (uint32_t*)dev_out);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 extern "C" int mastic_synchronize(mastic_ctx* c) {
     if (!c) return MASTIC_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -26,7 +26,7 @@ EXPORTS = [
     "mastic_reports_count", "mastic_reports_upload", "mastic_reports_download",
     "mastic_reports_shard", "mastic_prep_init", "mastic_prep_result", "mastic_aggregate",
     "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
-    "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats",
+    "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
 ]
 
 
@@ -114,6 +114,7 @@ def lib():
                     "mastic_last_timing": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
+                    "mastic_fold_shares": (i32, [P, P, sz, sz, P]),
                     "mastic_tree_stats": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64),
                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
                 }

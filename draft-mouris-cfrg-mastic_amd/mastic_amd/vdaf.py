@@ -210,6 +210,39 @@ class Mastic:
         _check(self._ctx, _lib.lib().mastic_aggregate(self._ctx, agg_id, _lib.buf(v), _lib.buf(out)))
         return self.field.decode_vec(out.tobytes())
 
+    # ------------------------------------------- device-resident batches
+    def reports_shard(self, ctx: bytes, alphas_packed: bytes, betas: bytes, nonces: bytes, rands: bytes):
+        """Shard n reports on the GPU and keep them resident in HBM."""
+        n = len(nonces) // 16
+        rep = Reports(self, n)
+        _check(self._ctx, _lib.lib().mastic_reports_shard(
+            rep._ptr, ctx, len(ctx), _lib.buf(alphas_packed), _lib.buf(betas), _lib.buf(nonces), _lib.buf(rands)))
+        return rep
+
+    def reports_upload(self, nonces: bytes, public_shares: bytes, input_shares_0=None, input_shares_1=None):
+        rep = Reports(self, len(nonces) // 16)
+        _check(self._ctx, _lib.lib().mastic_reports_upload(
+            rep._ptr, _lib.buf(nonces), _lib.buf(public_shares), _lib.buf(input_shares_0),
+            _lib.buf(input_shares_1)))
+        return rep
+
+    def prep_init_device(self, reports, verify_key: bytes, ctx: bytes, agg_id: int, agg_param):
+        """Enqueue prep_init for resident reports; results stay in HBM."""
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        _check(self._ctx, _lib.lib().mastic_prep_init(self._ctx, reports._ptr, verify_key, ctx, len(ctx), agg_id,
+                                                      enc, len(enc)))
+
+    def synchronize(self):
+        _check(self._ctx, _lib.lib().mastic_synchronize(self._ctx))
+
+    def last_timing(self):
+        """(eval_ms, eval_launches, absorb_ms, absorb_launches, total_ms) of the last prep_init."""
+        e, a, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        ne, na = ctypes.c_int(), ctypes.c_int()
+        _check(self._ctx, _lib.lib().mastic_last_timing(self._ctx, ctypes.byref(e), ctypes.byref(ne),
+                                                        ctypes.byref(a), ctypes.byref(na), ctypes.byref(t)))
+        return (e.value, ne.value, a.value, na.value, t.value)
+
     def tree_stats(self, agg_param):
         enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
@@ -413,6 +446,32 @@ class Mastic:
 
     def test_vec_encode_agg_share(self, agg_share) -> bytes:
         return self.field.encode_vec(agg_share) if len(agg_share) else b""
+
+
+class Reports:
+    """A batch of reports resident in HBM (wire encodings)."""
+
+    def __init__(self, mastic, n):
+        self._m = mastic
+        self._ptr = ctypes.c_void_p()
+        _check(mastic._ctx, _lib.lib().mastic_reports_create(mastic._ctx, n, ctypes.byref(self._ptr)))
+        self.n = n
+
+    def download(self):
+        m = self._m
+        n = self.n
+        nonces = np.empty(16 * n, np.uint8)
+        pub = np.empty(m.sizes.public_share_size * n, np.uint8)
+        in0 = np.empty(m.sizes.input_share_size[0] * n, np.uint8)
+        in1 = np.empty(m.sizes.input_share_size[1] * n, np.uint8)
+        _check(m._ctx, _lib.lib().mastic_reports_download(self._ptr, _lib.buf(nonces), _lib.buf(pub),
+                                                          _lib.buf(in0), _lib.buf(in1)))
+        return (nonces.tobytes(), pub.tobytes(), in0.tobytes(), in1.tobytes())
+
+    def __del__(self):
+        if getattr(self, "_ptr", None):
+            _lib.lib().mastic_reports_destroy(self._ptr)
+            self._ptr = None
 
 
 class MasticCount(Mastic):

@@ -125,6 +125,11 @@ int mastic_prep_result(mastic_ctx* ctx, int agg_id, uint8_t* prep_shares, uint8_
  * valid[i] != 0 (valid == NULL: all) into agg_share
  * (len(prefixes)*(1+output_len)*field_bytes, encode_vec). */
 int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t* agg_share);
+/* Multi-GPU merge (Mastic.merge, mastic.py:390-397) of n_shares agg shares
+ * of n_elems elements each, all in DEVICE memory of the ctx's GPU (e.g. the
+ * output of an RCCL all-gather): dev_out[e] = sum_s dev_shares[s][e] mod p.
+ * Elements are in encode_vec byte order. */
+int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares, size_t n_elems, void* dev_out);
 /* Wait for all enqueued work of the ctx. */
 int mastic_synchronize(mastic_ctx* ctx);
 
