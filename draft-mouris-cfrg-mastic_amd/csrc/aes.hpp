@@ -59,31 +59,49 @@ MH_D uint32_t b1(uint32_t x) { return __builtin_amdgcn_ubfe(x, 8, 8); }
 MH_D uint32_t b2(uint32_t x) { return __builtin_amdgcn_ubfe(x, 16, 8); }
 MH_D uint32_t b3(uint32_t x) { return x >> 24; }
 
-// Encrypt one block.  rk: 44 round-key words (little-endian column words).
-MH_D void aes128_encrypt(const AesLds& T, const uint32_t* rk, uint32_t s[4]) {
-    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+// Round-key sources: 44 words in registers, or a per-lane 176-byte row in LDS
+// read as one ds_read_b128 per round (rows of consecutive lanes are 176 B
+// apart: conflict-free for the b128 lane groups).
+struct RkRegs {
+    const uint32_t* k;
+    MH_D uint4 operator()(int round) const {
+        return uint4{k[4 * round], k[4 * round + 1], k[4 * round + 2], k[4 * round + 3]};
+    }
+};
+struct RkLds {
+    const uint4* row;
+    MH_D uint4 operator()(int round) const { return row[round]; }
+};
+
+// Encrypt one block.
+template <class RK>
+MH_D void aes128_encrypt(const AesLds& T, const RK& rk, uint32_t s[4]) {
+    uint4 k = rk(0);
+    uint32_t s0 = s[0] ^ k.x, s1 = s[1] ^ k.y, s2 = s[2] ^ k.z, s3 = s[3] ^ k.w;
 #pragma unroll
     for (int r = 1; r < 10; r++) {
+        k = rk(r);
         uint32_t t0 = xor3_u32(T.t0(b0(s0)), rot8(T.t0(b1(s1))), rot16(T.t0(b2(s2))));
         uint32_t t1 = xor3_u32(T.t0(b0(s1)), rot8(T.t0(b1(s2))), rot16(T.t0(b2(s3))));
         uint32_t t2 = xor3_u32(T.t0(b0(s2)), rot8(T.t0(b1(s3))), rot16(T.t0(b2(s0))));
         uint32_t t3 = xor3_u32(T.t0(b0(s3)), rot8(T.t0(b1(s0))), rot16(T.t0(b2(s1))));
-        t0 = xor3_u32(t0, rot24(T.t0(b3(s3))), rk[4 * r + 0]);
-        t1 = xor3_u32(t1, rot24(T.t0(b3(s0))), rk[4 * r + 1]);
-        t2 = xor3_u32(t2, rot24(T.t0(b3(s1))), rk[4 * r + 2]);
-        t3 = xor3_u32(t3, rot24(T.t0(b3(s2))), rk[4 * r + 3]);
+        t0 = xor3_u32(t0, rot24(T.t0(b3(s3))), k.x);
+        t1 = xor3_u32(t1, rot24(T.t0(b3(s0))), k.y);
+        t2 = xor3_u32(t2, rot24(T.t0(b3(s1))), k.z);
+        t3 = xor3_u32(t3, rot24(T.t0(b3(s2))), k.w);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    // Final round: S-box byte = byte 1 of T0 entry.  v_perm_b32 assembles it.
+    // Final round: S-box byte = byte 1 of the T0 entry.
+    k = rk(10);
     auto sb = [&](uint32_t x) { return b1(T.t0(x)); };
     uint32_t o0 = sb(b0(s0)) | (sb(b1(s1)) << 8) | (sb(b2(s2)) << 16) | (sb(b3(s3)) << 24);
     uint32_t o1 = sb(b0(s1)) | (sb(b1(s2)) << 8) | (sb(b2(s3)) << 16) | (sb(b3(s0)) << 24);
     uint32_t o2 = sb(b0(s2)) | (sb(b1(s3)) << 8) | (sb(b2(s0)) << 16) | (sb(b3(s1)) << 24);
     uint32_t o3 = sb(b0(s3)) | (sb(b1(s0)) << 8) | (sb(b2(s1)) << 16) | (sb(b3(s2)) << 24);
-    s[0] = o0 ^ rk[40];
-    s[1] = o1 ^ rk[41];
-    s[2] = o2 ^ rk[42];
-    s[3] = o3 ^ rk[43];
+    s[0] = o0 ^ k.x;
+    s[1] = o1 ^ k.y;
+    s[2] = o2 ^ k.z;
+    s[3] = o3 ^ k.w;
 }
 
 // AES-128 key expansion (FIPS-197 §5.2) with the S-box from the LDS table.
@@ -106,8 +124,8 @@ MH_D void aes128_expand(const AesLds& T, const uint32_t key[4], uint32_t rk[44])
 
 // XofFixedKeyAes128.hash_block for counter `ctr` (< 2^32 here):
 //   x = seed ^ le128(ctr); sigma(x) = x_hi || (x_hi ^ x_lo); out = AES(sigma) ^ sigma
-MH_D void fixed_key_block(const AesLds& T, const uint32_t* rk, const uint32_t seed[4], uint32_t ctr,
-                          uint32_t out[4]) {
+template <class RK>
+MH_D void fixed_key_block(const AesLds& T, const RK& rk, const uint32_t seed[4], uint32_t ctr, uint32_t out[4]) {
     uint32_t x0 = seed[0] ^ ctr, x1 = seed[1], x2 = seed[2], x3 = seed[3];
     uint32_t sg[4] = {x2, x3, x2 ^ x0, x3 ^ x1};
     uint32_t c[4] = {sg[0], sg[1], sg[2], sg[3]};
@@ -116,4 +134,66 @@ MH_D void fixed_key_block(const AesLds& T, const uint32_t* rk, const uint32_t se
     out[1] = c[1] ^ sg[1];
     out[2] = c[2] ^ sg[2];
     out[3] = c[3] ^ sg[3];
+}
+MH_D void fixed_key_block(const AesLds& T, const uint32_t* rk, const uint32_t seed[4], uint32_t ctr,
+                          uint32_t out[4]) {
+    fixed_key_block(T, RkRegs{rk}, seed, ctr, out);
+}
+
+// Two independent blocks in lockstep, round by round: one wave then always has
+// 32 independent T-table lookups in flight instead of 16, which hides the LDS
+// latency of one chain behind the other (both use the same key schedule).
+template <class RK>
+MH_D void aes128_encrypt2(const AesLds& T, const RK& rk, uint32_t a[4], uint32_t b[4]) {
+    uint4 k = rk(0);
+    uint32_t a0 = a[0] ^ k.x, a1 = a[1] ^ k.y, a2 = a[2] ^ k.z, a3 = a[3] ^ k.w;
+    uint32_t c0 = b[0] ^ k.x, c1 = b[1] ^ k.y, c2 = b[2] ^ k.z, c3 = b[3] ^ k.w;
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k = rk(r);
+        uint32_t t0 = xor3_u32(T.t0(b0(a0)), rot8(T.t0(b1(a1))), rot16(T.t0(b2(a2))));
+        uint32_t u0 = xor3_u32(T.t0(b0(c0)), rot8(T.t0(b1(c1))), rot16(T.t0(b2(c2))));
+        uint32_t t1 = xor3_u32(T.t0(b0(a1)), rot8(T.t0(b1(a2))), rot16(T.t0(b2(a3))));
+        uint32_t u1 = xor3_u32(T.t0(b0(c1)), rot8(T.t0(b1(c2))), rot16(T.t0(b2(c3))));
+        uint32_t t2 = xor3_u32(T.t0(b0(a2)), rot8(T.t0(b1(a3))), rot16(T.t0(b2(a0))));
+        uint32_t u2 = xor3_u32(T.t0(b0(c2)), rot8(T.t0(b1(c3))), rot16(T.t0(b2(c0))));
+        uint32_t t3 = xor3_u32(T.t0(b0(a3)), rot8(T.t0(b1(a0))), rot16(T.t0(b2(a1))));
+        uint32_t u3 = xor3_u32(T.t0(b0(c3)), rot8(T.t0(b1(c0))), rot16(T.t0(b2(c1))));
+        t0 = xor3_u32(t0, rot24(T.t0(b3(a3))), k.x);
+        u0 = xor3_u32(u0, rot24(T.t0(b3(c3))), k.x);
+        t1 = xor3_u32(t1, rot24(T.t0(b3(a0))), k.y);
+        u1 = xor3_u32(u1, rot24(T.t0(b3(c0))), k.y);
+        t2 = xor3_u32(t2, rot24(T.t0(b3(a1))), k.z);
+        u2 = xor3_u32(u2, rot24(T.t0(b3(c1))), k.z);
+        t3 = xor3_u32(t3, rot24(T.t0(b3(a2))), k.w);
+        u3 = xor3_u32(u3, rot24(T.t0(b3(c2))), k.w);
+        a0 = t0; a1 = t1; a2 = t2; a3 = t3;
+        c0 = u0; c1 = u1; c2 = u2; c3 = u3;
+    }
+    k = rk(10);
+    auto sb = [&](uint32_t x) { return b1(T.t0(x)); };
+    a[0] = (sb(b0(a0)) | (sb(b1(a1)) << 8) | (sb(b2(a2)) << 16) | (sb(b3(a3)) << 24)) ^ k.x;
+    b[0] = (sb(b0(c0)) | (sb(b1(c1)) << 8) | (sb(b2(c2)) << 16) | (sb(b3(c3)) << 24)) ^ k.x;
+    a[1] = (sb(b0(a1)) | (sb(b1(a2)) << 8) | (sb(b2(a3)) << 16) | (sb(b3(a0)) << 24)) ^ k.y;
+    b[1] = (sb(b0(c1)) | (sb(b1(c2)) << 8) | (sb(b2(c3)) << 16) | (sb(b3(c0)) << 24)) ^ k.y;
+    a[2] = (sb(b0(a2)) | (sb(b1(a3)) << 8) | (sb(b2(a0)) << 16) | (sb(b3(a1)) << 24)) ^ k.z;
+    b[2] = (sb(b0(c2)) | (sb(b1(c3)) << 8) | (sb(b2(c0)) << 16) | (sb(b3(c1)) << 24)) ^ k.z;
+    a[3] = (sb(b0(a3)) | (sb(b1(a0)) << 8) | (sb(b2(a1)) << 16) | (sb(b3(a2)) << 24)) ^ k.w;
+    b[3] = (sb(b0(c3)) | (sb(b1(c0)) << 8) | (sb(b2(c1)) << 16) | (sb(b3(c2)) << 24)) ^ k.w;
+}
+
+// Two fixed-key blocks (seed_a, ctr_a) and (seed_b, ctr_b) in lockstep.
+template <class RK>
+MH_D void fixed_key_block2(const AesLds& T, const RK& rk, const uint32_t sa[4], uint32_t ca, const uint32_t sb_[4],
+                           uint32_t cb, uint32_t oa[4], uint32_t ob[4]) {
+    uint32_t ga[4] = {sa[2], sa[3], sa[2] ^ sa[0] ^ ca, sa[3] ^ sa[1]};
+    uint32_t gb[4] = {sb_[2], sb_[3], sb_[2] ^ sb_[0] ^ cb, sb_[3] ^ sb_[1]};
+    uint32_t xa[4] = {ga[0], ga[1], ga[2], ga[3]};
+    uint32_t xb[4] = {gb[0], gb[1], gb[2], gb[3]};
+    aes128_encrypt2(T, rk, xa, xb);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        oa[i] = xa[i] ^ ga[i];
+        ob[i] = xb[i] ^ gb[i];
+    }
 }

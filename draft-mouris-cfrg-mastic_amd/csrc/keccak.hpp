@@ -77,7 +77,9 @@ MH_D void kxor_word(KState& s, int j, uint32_t v) {  // j compile-time constant
 // Absorb `nbytes` body bytes given as little-endian 32-bit words ld(m),
 // m in [0, ceil(nbytes/4)), into a sponge currently filled up to byte f of its
 // block.  f is uniform.  Bytes of the last word past nbytes must be zero.
-// Returns the new fill position.
+// Returns the new fill position.  Branch-free: out-of-range words are loaded
+// from a clamped index and replaced by zero with a uniform select, so the
+// state never sits live across dozens of tiny basic blocks.
 template <class Loader>
 MH_D int sponge_absorb_words(KState& s, int f, int nbytes, Loader ld) {
     if (nbytes <= 0) return f;
@@ -85,13 +87,18 @@ MH_D int sponge_absorb_words(KState& s, int f, int nbytes, Loader ld) {
     const int sh = f & 3;
     const int nw = (nbytes + 3) >> 2;
     const int end = f + nbytes;
+    auto get = [&](int m) {
+        const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
+        const uint32_t v = ld(mc);
+        return (m >= 0 && m < nw) ? v : 0u;
+    };
     for (int b = 0;; b++) {
         const int base = KECCAK_RATE_WORDS * b - q;
-        uint32_t prev = (base - 1 >= 0 && base - 1 < nw) ? ld(base - 1) : 0u;
+        uint32_t prev = get(base - 1);
 #pragma unroll
         for (int j = 0; j < KECCAK_RATE_WORDS; j++) {
             const int m = base + j;
-            uint32_t cur = (m >= 0 && m < nw) ? ld(m) : 0u;
+            uint32_t cur = get(m);
             uint32_t w = sh ? __builtin_amdgcn_alignbit(cur, prev, 32 - 8 * sh) : cur;
             prev = cur;
             kxor_word(s, j, w);
@@ -110,8 +117,7 @@ MH_D void sponge_pad(KState& s, int f, uint32_t domain) {
     const int q = f >> 2;
     const uint32_t dw = domain << (8 * (f & 3));
 #pragma unroll
-    for (int j = 0; j < KECCAK_RATE_WORDS; j++)
-        if (j == q) kxor_word(s, j, dw);
+    for (int j = 0; j < KECCAK_RATE_WORDS; j++) kxor_word(s, j, j == q ? dw : 0u);
     s.a[20].hi ^= 0x80000000u;
     keccak_p12(s);
 }

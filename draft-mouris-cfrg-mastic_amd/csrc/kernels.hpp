@@ -198,7 +198,20 @@ template <> struct ConvStream<F64> {
         ctr = 1;
         half = 2;
     }
-    MH_D uint64_t next(const AesLds& T, const uint32_t* rk) {
+    // Common case: both children's streams need their next block at the same
+    // element (no rejection so far): produce both in one paired AES call.
+    template <class RK>
+    MH_D void refill_pair(ConvStream& o, const AesLds& T, const RK& rk) {
+        if (half == 2 && o.half == 2) {
+            fixed_key_block2(T, rk, seed, ctr, o.seed, o.ctr, blk, o.blk);
+            ctr++;
+            o.ctr++;
+            half = 0;
+            o.half = 0;
+        }
+    }
+    template <class RK>
+    MH_D uint64_t next(const AesLds& T, const RK& rk) {
         uint64_t v;
         do {
             if (half == 2) {
@@ -215,18 +228,34 @@ template <> struct ConvStream<F64> {
 
 template <> struct ConvStream<F128> {
     uint32_t seed[4];
+    uint32_t blk[4];
     uint32_t ctr;
+    uint32_t have;  // blk holds an unconsumed candidate
     MH_D void init(const uint32_t s[4]) {
         seed[0] = s[0]; seed[1] = s[1]; seed[2] = s[2]; seed[3] = s[3];
         ctr = 1;
+        have = 0;
     }
-    MH_D F128::E next(const AesLds& T, const uint32_t* rk) {
+    template <class RK>
+    MH_D void refill_pair(ConvStream& o, const AesLds& T, const RK& rk) {
+        if (!have && !o.have) {
+            fixed_key_block2(T, rk, seed, ctr, o.seed, o.ctr, blk, o.blk);
+            ctr++;
+            o.ctr++;
+            have = 1;
+            o.have = 1;
+        }
+    }
+    template <class RK>
+    MH_D F128::E next(const AesLds& T, const RK& rk) {
         F128::E v;
         do {
-            uint32_t b[4];
-            fixed_key_block(T, rk, seed, ctr, b);
-            ctr++;
-            v = F128::from_words(b);
+            if (!have) {
+                fixed_key_block(T, rk, seed, ctr, blk);
+                ctr++;
+            }
+            have = 0;
+            v = F128::from_words(blk);
         } while (!F128::valid(v));
         return v;
     }
@@ -254,20 +283,36 @@ struct LevelArgs {
     uint32_t* onehot;    // [2 * n_parents * 8]   node proofs of this level (BFS order)
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
+    PrefixState np;      // node-proof sponge prefix (kernel argument -> SGPRs)
+    const PrefixState* npp;  // the same state in device memory
 };
 
+// One workgroup = 64 reports (one per lane) x 4 waves, each wave walking its
+// own run of parents.  LDS: the replicated T-table (32 KiB), the 64 reports'
+// two AES key schedules (22 KiB, one ds_read_b128 per round) and the
+// node-proof message staging (16 KiB).
 template <class F>
-__global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, LevelArgs a, const PrefixState* pfx) {
+__global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, LevelArgs a) {
     typedef typename F::E E;
     __shared__ uint32_t T[AES_LDS_WORDS];
     __shared__ uint32_t V[16 * 256];  // node-proof message staging, [word][thread]
+    __shared__ uint4 RKE[64 * 11];
+    __shared__ uint4 RKC[64 * 11];
     aes_lds_fill(T, threadIdx.x, 256);
-    __syncthreads();
 
     const int S = pl.stride;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = blockIdx.x * 64 + lane;
+    {
+        uint32_t* ke = (uint32_t*)RKE;
+        uint32_t* kc = (uint32_t*)RKC;
+        for (int i = wave; i < 44; i += 4) {
+            ke[lane * 44 + i] = pl.rk_ext[i * S + r];
+            kc[lane * 44 + i] = pl.rk_conv[i * S + r];
+        }
+    }
+    __syncthreads();
     const int pbeg = (blockIdx.y * 4 + wave) * a.ppw;
     if (pbeg >= a.n_parents) return;
     const int pend = min(pbeg + a.ppw, a.n_parents);
@@ -275,22 +320,13 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
     const int vl = p.value_len;
     const int wl = vl * F::W32;
     AesLds TL{T + (lane & 31)};
-
-    uint32_t rke[44], rkc[44];
-#pragma unroll
-    for (int i = 0; i < 44; i++) {
-        rke[i] = pl.rk_ext[i * S + r];
-        rkc[i] = pl.rk_conv[i * S + r];
-    }
+    const RkLds rke{RKE + lane * 11};
+    const RkLds rkc{RKC + lane * 11};
     uint32_t scw[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) scw[i] = pl.cw_seed[((size_t)l * 4 + i) * S + r];
     const uint32_t ccw = pl.cw_ctrl[(size_t)l * S + r];
     const uint32_t* wcw = pl.cw_w + (size_t)l * wl * S;
-
-    KState s0;
-    int f0;
-    load_prefix(pfx, PFX_NODE, s0, f0);
 
     for (int pi = pbeg; pi < pend; pi++) {
         // parent seed / control bit
@@ -305,42 +341,39 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
             for (int i = 0; i < 4; i++) ps[i] = a.fr_seed_in[((size_t)pi * 4 + i) * S + r];
             pctrl = a.fr_ctrl_in[(size_t)pi * S + r];
         }
-        // extend (block c belongs to child c) + correct, then the convert seed block
-        uint32_t cs[2][4], ns[2][4], tc[2];
-#pragma unroll 1
-        for (int c = 0; c < 2; c++) {
-            uint32_t b[4];
-            fixed_key_block(TL, rke, ps, (uint32_t)c, b);
-            uint32_t t = b[0] & 1u;
-            b[0] &= ~1u;
-            if (pctrl) {
-                b[0] ^= scw[0]; b[1] ^= scw[1]; b[2] ^= scw[2]; b[3] ^= scw[3];
-                t ^= (ccw >> c) & 1u;
-            }
-            uint32_t nb[4];
-            fixed_key_block(TL, rkc, b, 0u, nb);
+        // extend: block 0 -> left child, block 1 -> right child (one paired
+        // AES call), correct, then both children's convert seed blocks.
+        uint32_t cs0[4], cs1[4], ns0[4], ns1[4];
+        fixed_key_block2(TL, rke, ps, 0u, ps, 1u, cs0, cs1);
+        uint32_t tc0 = cs0[0] & 1u, tc1 = cs1[0] & 1u;
+        cs0[0] &= ~1u;
+        cs1[0] &= ~1u;
+        if (pctrl) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                cs[c][i] = b[i];
-                ns[c][i] = nb[i];
+                cs0[i] ^= scw[i];
+                cs1[i] ^= scw[i];
             }
-            tc[c] = t;
+            tc0 ^= ccw & 1u;
+            tc1 ^= (ccw >> 1) & 1u;
         }
+        fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
 
         // payloads of both children, element by element
         ConvStream<F> st0, st1;
-        st0.init(cs[0]);
-        st1.init(cs[1]);
+        st0.init(cs0);
+        st1.init(cs1);
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         const int row = 1 + p.output_len;
         for (int e = 0; e < vl; e++) {
+            st0.refill_pair(st1, TL, rkc);
             E x0 = st0.next(TL, rkc);
             E x1 = st1.next(TL, rkc);
             E cw = pl_load<F>(wcw, e, S, r);
-            if (tc[0]) x0 = F::add(x0, cw);
-            if (tc[1]) x1 = F::add(x1, cw);
+            if (tc0) x0 = F::add(x0, cw);
+            if (tc1) x1 = F::add(x1, cw);
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
             if (l == 0) {
@@ -378,18 +411,24 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
 #pragma unroll 1
         for (int c = 0; c < 2; c++) {
             const int node = 2 * pi + c;
-            V[0 * 256 + threadIdx.x] = ns[c][0];
-            V[1 * 256 + threadIdx.x] = ns[c][1];
-            V[2 * 256 + threadIdx.x] = ns[c][2];
-            V[3 * 256 + threadIdx.x] = ns[c][3];
+            uint32_t nsc[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                nsc[i] = c ? ns1[i] : ns0[i];
+                V[i * 256 + threadIdx.x] = nsc[i];
+            }
             V[4 * 256 + threadIdx.x] = (uint32_t)p.bits | ((uint32_t)l << 16);
             const int pw = (a.path_bytes + 3) >> 2;
             for (int i = 0; i < pw; i++) V[(5 + i) * 256 + threadIdx.x] = a.child_path[node * 8 + i];
-            KState s = s0;
-            int f = sponge_absorb_words(s, f0, 20 + a.path_bytes,
+            // Re-read the (uniform) prefix state for every proof instead of
+            // pinning 50 loop-invariant registers across the parent loop.
+            asm volatile("" ::: "memory");
+            KState s = a.npp->st;
+            int f = sponge_absorb_words(s, a.np.f, 20 + a.path_bytes,
                                         [&](int m) { return V[m * 256 + threadIdx.x]; });
             sponge_pad(s, f, 0x01);
-            const bool t = tc[c] != 0;
+            const uint32_t tcc = c ? tc1 : tc0;
+            const bool t = tcc != 0;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 uint32_t w = kword(s, j);
@@ -399,8 +438,8 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
             const int ce = c ? ce1 : ce0;
             if (ce >= 0) {
 #pragma unroll
-                for (int i = 0; i < 4; i++) a.fr_seed_out[((size_t)ce * 4 + i) * S + r] = ns[c][i];
-                a.fr_ctrl_out[(size_t)ce * S + r] = tc[c];
+                for (int i = 0; i < 4; i++) a.fr_seed_out[((size_t)ce * 4 + i) * S + r] = nsc[i];
+                a.fr_ctrl_out[(size_t)ce * S + r] = tcc;
             }
         }
     }
@@ -415,6 +454,8 @@ struct AbsorbArgs {
     int f[2];
 };
 
+// The next block's 43 source words are loaded before the current block's
+// permutation, so their HBM/L2 latency hides under ~2.3k VALU instructions.
 __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     const int which = blockIdx.y;
@@ -427,7 +468,37 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     KState s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = u32x2{sp[(2 * i) * S + r], sp[(2 * i + 1) * S + r]};
-    sponge_absorb_words(s, a.f[which], nb, [&](int m) { return seg[(size_t)m * S + r]; });
+    const int f = a.f[which];
+    const int q = f >> 2;
+    const int sh = f & 3;
+    const int nw = (nb + 3) >> 2;
+    const int end = f + nb;
+    auto load_block = [&](int b, uint32_t* w) {
+        const int base = KECCAK_RATE_WORDS * b - q - 1;
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
+            const int m = base + j;
+            const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
+            const uint32_t v = seg[(size_t)mc * S + r];
+            w[j] = (m >= 0 && m < nw) ? v : 0u;
+        }
+    };
+    uint32_t cur[KECCAK_RATE_WORDS + 1];
+    load_block(0, cur);
+    for (int b = 0;; b++) {
+        const bool full = end >= KECCAK_RATE * (b + 1);
+        const bool more = end > KECCAK_RATE * (b + 1);
+        uint32_t nxt[KECCAK_RATE_WORDS + 1];
+        if (more) load_block(b + 1, nxt);
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS; j++)
+            kxor_word(s, j, sh ? __builtin_amdgcn_alignbit(cur[j + 1], cur[j], 32 - 8 * sh) : cur[j + 1]);
+        if (!full) break;
+        keccak_p12(s);
+        if (!more) break;
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) cur[j] = nxt[j];
+    }
 #pragma unroll
     for (int i = 0; i < 25; i++) {
         sp[(2 * i) * S + r] = s.a[i].lo;

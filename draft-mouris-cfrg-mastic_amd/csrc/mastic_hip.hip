@@ -77,7 +77,10 @@ struct mastic_ctx {
     mastic_params user{};
     McParams p{};
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // level evals, setup, finalize, FLP
+    hipStream_t stream2 = nullptr;  // binder sponges (overlap the next level's eval)
+    std::vector<hipEvent_t> sync_ev;
+    PrefixState pfx_host[PFX_COUNT];
     std::string err;
     uint64_t budget = 0;
     DevBuf work;     // per-chunk planes
@@ -94,7 +97,9 @@ struct mastic_ctx {
     ~mastic_ctx() {
         for (auto& kv : trees) delete kv.second;
         for (auto e : ev) (void)hipEventDestroy(e);
+        for (auto e : sync_ev) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
+        if (stream2) (void)hipStreamDestroy(stream2);
     }
 };
 
@@ -181,7 +186,8 @@ static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len,
                        c->pfx_meta.as<int>(), c->pfx_meta.as<int>() + PFX_COUNT, (int)PFX_COUNT,
                        c->pfx.as<PrefixState>());
     HIPCHK(c, hipGetLastError());
-    // pfx_bytes must outlive the async kernel: keep it until the next call.
+    HIPCHK(c, hipMemcpyAsync(c->pfx_host, c->pfx.p, sizeof(PrefixState) * PFX_COUNT, hipMemcpyDeviceToHost,
+                             c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -325,8 +331,9 @@ struct WorkLayout {
     size_t words = 0;  // per report (plane count)
     size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
         rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, fr_seed[2], fr_ctrl[2],
-        fr_w[2], onehot, payload, out;
+        fr_w[2], onehot[3], payload[3], out;
 };
+static constexpr int NSLOT = 3;  // level buffers in flight between eval and absorb
 
 static WorkLayout work_layout(const McParams& p, const Tree* t) {
     WorkLayout w;
@@ -365,8 +372,10 @@ static WorkLayout work_layout(const McParams& p, const Tree* t) {
         w.fr_ctrl[s] = take(std::max(t->max_exp, 1));
         w.fr_w[s] = take((size_t)std::max(t->max_exp, 1) * wl);
     }
-    w.onehot = take((size_t)t->max_level_nodes * 8);
-    w.payload = take((size_t)t->max_parents * wl);
+    for (int k = 0; k < NSLOT; k++) {
+        w.onehot[k] = take((size_t)t->max_level_nodes * 8);
+        w.payload[k] = take((size_t)t->max_parents * wl);
+    }
     w.out = take((size_t)std::max(t->n_prefixes, 1) * (1 + p.output_len) * p.w32);
     w.words = o;
     return w;
@@ -401,6 +410,15 @@ static Planes make_planes(uint32_t* base, const WorkLayout& w, int n, int stride
     pl.verifier = P(w.verifier);
     pl.status = (int32_t*)P(w.status);
     return pl;
+}
+
+static hipEvent_t get_sync_event(mastic_ctx* c, size_t i) {
+    while (c->sync_ev.size() <= i) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        c->sync_ev.push_back(e);
+    }
+    return c->sync_ev[i];
 }
 
 static hipEvent_t get_event(mastic_ctx* c, size_t i) {
@@ -447,7 +465,13 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const int wlw = p.value_len * p.w32;
     int f_oh = c->pfx_f[PFX_ONEHOT], f_pl = c->pfx_f[PFX_PAYLOAD];
     auto plane = [&](size_t off) { return W + off * (size_t)stride; };
+    // eval of level l+1.. runs while the binder sponges absorb level l: the
+    // sponges are serial per report (latency-bound), the evals fill the chip.
+    size_t sev = 0;
+    std::vector<hipEvent_t> abs_done(t->L + 1);
     for (int l = 0; l <= t->L; l++) {
+        const int slot = l % NSLOT;
+        if (l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
         LevelArgs a;
         a.level = l;
         a.last_level = t->L;
@@ -466,15 +490,19 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.fr_seed_out = plane(wl.fr_seed[sout]);
         a.fr_ctrl_out = plane(wl.fr_ctrl[sout]);
         a.fr_w_out = plane(wl.fr_w[sout]);
-        a.onehot = plane(wl.onehot);
-        a.payload = plane(wl.payload);
+        a.onehot = plane(wl.onehot[slot]);
+        a.payload = plane(wl.payload[slot]);
         a.out = plane(wl.out);
+        a.np = c->pfx_host[PFX_NODE];
+        a.npp = (const PrefixState*)c->pfx.p + PFX_NODE;
         dim3 grid(groups, (a.n_parents + 4 * a.ppw - 1) / (4 * a.ppw));
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        hipLaunchKernelGGL(k_eval_level<F>, grid, dim3(256), 0, c->stream, p, pl, a, pfx);
+        hipLaunchKernelGGL(k_eval_level<F>, grid, dim3(256), 0, c->stream, p, pl, a);
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipGetLastError());
+        hipEvent_t ev_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(ev_done, c->stream));
 
         AbsorbArgs ab;
         ab.seg[0] = a.onehot;
@@ -483,14 +511,18 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         ab.seg[1] = a.payload;
         ab.nbytes[1] = l > 0 ? a.n_parents * wlw * 4 : 0;
         ab.f[1] = f_pl;
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, ev_done, 0));
         hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
-        HIPCHK(c, hipEventRecord(e2, c->stream));
-        hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream, pl, ab);
-        HIPCHK(c, hipEventRecord(e3, c->stream));
+        HIPCHK(c, hipEventRecord(e2, c->stream2));
+        hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
+        HIPCHK(c, hipEventRecord(e3, c->stream2));
         HIPCHK(c, hipGetLastError());
+        abs_done[l] = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(abs_done[l], c->stream2));
         f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
         f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
     }
+    HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
     hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl, fa, pfx);
     if (t->weight_check) {
@@ -741,6 +773,14 @@ extern "C" int mastic_tree_stats(mastic_ctx* c, const uint8_t* enc, size_t len, 
     return 0;
 }
 
+extern "C" int mastic_work_bytes(mastic_ctx* c, const uint8_t* enc, size_t len, uint64_t* per_report) {
+    Tree* t = nullptr;
+    int rc = build_tree(c, enc, len, &t);
+    if (rc) return rc;
+    if (per_report) *per_report = (uint64_t)work_layout(c->p, t).words * 4;
+    return 0;
+}
+
 extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t verify_key[32], const uint8_t* app_ctx,
                                       size_t ctx_len, int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len,
                                       size_t n, const uint8_t* nonces, const uint8_t* public_shares,
@@ -967,7 +1007,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->user = *up;
     c->p = p;
     c->device = up->device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MASTIC_EHIP;
     }

@@ -80,12 +80,13 @@ __global__ __launch_bounds__(256) void k_shard(McParams p, ShardArgs a, const Pr
         uint32_t* dst = which == 0 ? a.rke : a.rkc;
         for (int i = 0; i < 44; i++) dst[i * S + r] = rk[i];
     }
-    uint32_t rke[44], rkc[44];
+    uint32_t rke_w[44], rkc_w[44];
 #pragma unroll
     for (int i = 0; i < 44; i++) {
-        rke[i] = a.rke[i * S + r];
-        rkc[i] = a.rkc[i * S + r];
+        rke_w[i] = a.rke[i * S + r];
+        rkc_w[i] = a.rkc[i * S + r];
     }
+    const RkRegs rke{rke_w}, rkc{rkc_w};
     KState s0;
     int f0;
     load_prefix(pfx, PFX_NODE, s0, f0);

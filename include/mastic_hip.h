@@ -164,6 +164,9 @@ int mastic_shard_batch(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_len, 
  * stream; also their launch counts. */
 int mastic_last_timing(mastic_ctx* ctx, double* eval_ms, int* eval_launches, double* absorb_ms,
                        int* absorb_launches, double* total_ms);
+/* HBM work-buffer bytes one report needs during prep_init with this agg
+ * param (prep_init processes reports in chunks of budget / this). */
+int mastic_work_bytes(mastic_ctx* ctx, const uint8_t* enc_agg_param, size_t agg_param_len, uint64_t* per_report);
 /* Tree statistics of an encoded agg param: nodes evaluated per report,
  * interior nodes, max nodes on one level. */
 int mastic_tree_stats(mastic_ctx* ctx, const uint8_t* enc_agg_param, size_t agg_param_len, uint64_t* nodes,

@@ -246,10 +246,13 @@ def test_chunked_batches_equal_unchunked(mastic_amd):
     vk = bytes(32)
     full = m.prep_init_batch(vk, CTX, 0, ap, nonces, pub, in0)
     agg_full = m.aggregate_device(0, ap)
+    import ctypes
     from mastic_amd import _lib
+    enc = m.encode_agg_param(ap)
+    per = ctypes.c_uint64()
+    assert _lib.lib().mastic_work_bytes(m._ctx, enc, len(enc), ctypes.byref(per)) == 0
     try:
-        # ~5 KB of work planes per report here: a 400 KB budget -> 64-report chunks
-        _lib.lib().mastic_set_memory_budget(m._ctx, 400_000)
+        _lib.lib().mastic_set_memory_budget(m._ctx, 64 * per.value + 1000)  # -> 64-report chunks
         m2 = m.prep_init_batch(vk, CTX, 0, ap, nonces, pub, in0)
     finally:
         _lib.lib().mastic_set_memory_budget(m._ctx, 0)
