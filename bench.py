@@ -114,8 +114,8 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from mastic_amd import MasticSum, _lib
-    import ctypes
+    from mastic_amd import MasticSum
+    from mastic_amd.merge import merge_agg_shares
 
     m = MasticSum(32, 255, device=local)
     ctx = b"mastic-mi355x-bench"
@@ -125,20 +125,12 @@ def main():
     enc_ap = agg_param_bytes(attrs)
     reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
     (nodes, interior, _maxl) = m.tree_stats(enc_ap)
-    n_elems = len(attrs) * (1 + m.OUTPUT_LEN)
 
     def step():
         m.prep_init_device(reps, vk, ctx, args.agg_id, enc_ap)
         agg = m.aggregate_device(args.agg_id, enc_ap)
         if world > 1:
-            local_share = torch.frombuffer(bytearray(m.field.encode_vec(agg)), dtype=torch.uint8).cuda()
-            gathered = torch.empty(world * local_share.numel(), dtype=torch.uint8, device="cuda")
-            dist.all_gather_into_tensor(gathered, local_share)
-            merged = torch.empty_like(local_share)
-            torch.cuda.synchronize()
-            rc = _lib.lib().mastic_fold_shares(m._ctx, ctypes.c_void_p(gathered.data_ptr()), world, n_elems,
-                                               ctypes.c_void_p(merged.data_ptr()))
-            assert rc == 0, rc
+            merge_agg_shares(m, agg, dist)  # RCCL all-gather + on-GPU mod-p fold
         return agg
 
     for _ in range(args.warmup):
