@@ -85,24 +85,26 @@ MH_D int sponge_absorb_words(KState& s, int f, int nbytes, Loader ld) {
     if (nbytes <= 0) return f;
     const int q = f >> 2;
     const int sh = f & 3;
+    const int off = sh ? 1 : 0;
+    const int amt = (32 - 8 * sh) & 31;
     const int nw = (nbytes + 3) >> 2;
     const int end = f + nbytes;
-    auto get = [&](int m) {
-        const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-        const uint32_t v = ld(mc);
-        return (m >= 0 && m < nw) ? v : 0u;
-    };
     for (int b = 0;; b++) {
-        const int base = KECCAK_RATE_WORDS * b - q;
-        uint32_t prev = get(base - 1);
+        const int base = KECCAK_RATE_WORDS * b - q - off;
+        uint32_t w[KECCAK_RATE_WORDS + 1];
+        // all loads first (clamped index), then the uniform zero-selects
 #pragma unroll
-        for (int j = 0; j < KECCAK_RATE_WORDS; j++) {
+        for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
             const int m = base + j;
-            uint32_t cur = get(m);
-            uint32_t w = sh ? __builtin_amdgcn_alignbit(cur, prev, 32 - 8 * sh) : cur;
-            prev = cur;
-            kxor_word(s, j, w);
+            w[j] = ld(m < 0 ? 0 : (m >= nw ? nw - 1 : m));
         }
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
+            const int m = base + j;
+            w[j] = (m >= 0 && m < nw) ? w[j] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < KECCAK_RATE_WORDS; j++) kxor_word(s, j, __builtin_amdgcn_alignbit(w[j + 1], w[j], amt));
         if (end >= KECCAK_RATE * (b + 1)) {
             keccak_p12(s);
             if (end == KECCAK_RATE * (b + 1)) return 0;

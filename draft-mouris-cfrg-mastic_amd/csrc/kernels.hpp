@@ -456,7 +456,13 @@ struct AbsorbArgs {
 
 // The next block's 43 source words are loaded before the current block's
 // permutation, so their HBM/L2 latency hides under ~2.3k VALU instructions.
+// Blocks whose words are all in range (every block but the first and last of
+// a launch) use plain loads: a zero-select right after a load would force a
+// vmcnt(0) wait per word.
 __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
+    // The sponge chain is the latency-critical path and runs beside the
+    // level-eval waves: win every issue arbitration on the shared SIMD.
+    __builtin_amdgcn_s_setprio(3);
     const int r = blockIdx.x * 256 + threadIdx.x;
     const int which = blockIdx.y;
     if (r >= pl.stride) return;
@@ -464,23 +470,35 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     if (nb == 0) return;
     const int S = pl.stride;
     uint32_t* sp = which == 0 ? pl.sp_onehot : pl.sp_payload;
-    const uint32_t* seg = a.seg[which];
+    const uint32_t* seg = a.seg[which] + r;
     KState s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = u32x2{sp[(2 * i) * S + r], sp[(2 * i + 1) * S + r]};
     const int f = a.f[which];
     const int q = f >> 2;
     const int sh = f & 3;
+    const int off = sh ? 1 : 0;           // window starts one word early when shifted
+    const int amt = (32 - 8 * sh) & 31;  // block word j = alignbit(w[j+1], w[j], amt)
     const int nw = (nb + 3) >> 2;
     const int end = f + nb;
     auto load_block = [&](int b, uint32_t* w) {
-        const int base = KECCAK_RATE_WORDS * b - q - 1;
+        const int base = KECCAK_RATE_WORDS * b - q - off;
+        if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
+            const uint32_t* p = seg + (size_t)base * S;
 #pragma unroll
-        for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
-            const int m = base + j;
-            const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-            const uint32_t v = seg[(size_t)mc * S + r];
-            w[j] = (m >= 0 && m < nw) ? v : 0u;
+            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) w[j] = p[(size_t)j * S];
+        } else {
+#pragma unroll
+            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
+                const int m = base + j;
+                const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
+                w[j] = seg[(size_t)mc * S];
+            }
+#pragma unroll
+            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
+                const int m = base + j;
+                w[j] = (m >= 0 && m < nw) ? w[j] : 0u;
+            }
         }
     };
     uint32_t cur[KECCAK_RATE_WORDS + 1];
@@ -491,8 +509,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
         uint32_t nxt[KECCAK_RATE_WORDS + 1];
         if (more) load_block(b + 1, nxt);
 #pragma unroll
-        for (int j = 0; j < KECCAK_RATE_WORDS; j++)
-            kxor_word(s, j, sh ? __builtin_amdgcn_alignbit(cur[j + 1], cur[j], 32 - 8 * sh) : cur[j + 1]);
+        for (int j = 0; j < KECCAK_RATE_WORDS; j++) kxor_word(s, j, __builtin_amdgcn_alignbit(cur[j + 1], cur[j], amt));
         if (!full) break;
         keccak_p12(s);
         if (!more) break;
