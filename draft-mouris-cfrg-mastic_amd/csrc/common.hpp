@@ -33,3 +33,22 @@ MH_D u32x2 xor64(u32x2 a, u32x2 b) { return u32x2{a.lo ^ b.lo, a.hi ^ b.hi}; }
 MH_D u32x2 xor3_64(u32x2 a, u32x2 b, u32x2 c) {
     return u32x2{xor3_u32(a.lo, b.lo, c.lo), xor3_u32(a.hi, b.hi, c.hi)};
 }
+
+// Plane access through buffer resources: the base address is wave-uniform
+// (kernel arguments + uniform indices) and lives in an SGPR descriptor; the
+// only per-lane part is the 32-bit byte offset of the lane's report.  One VGPR
+// serves every plane access instead of a 64-bit pointer per access stream
+// (cdna_hip_programming.md T8/T20: readfirstlane makes uniformity provable).
+MH_D __amdgpu_buffer_rsrc_t mh_rsrc(const void* p) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, 0x7fffffff, 0x00020000);
+}
+// load / store word `lane_bytes / 4` of the plane starting at uniform address p
+MH_D uint32_t pld(const uint32_t* p, uint32_t lane_bytes) {
+    return __builtin_amdgcn_raw_buffer_load_b32(mh_rsrc(p), lane_bytes, 0, 0);
+}
+MH_D void pst(uint32_t* p, uint32_t lane_bytes, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, mh_rsrc(p), lane_bytes, 0, 0);
+}

@@ -13,17 +13,18 @@
 #include "params.hpp"
 
 // Element load/store on word planes.
+// plane0 and elt must be wave-uniform; r is the lane's report (column).
 template <class F>
 MH_D typename F::E pl_load(const uint32_t* plane0, int elt, int stride, int r) {
     uint32_t w[F::W32];
 #pragma unroll
-    for (int i = 0; i < F::W32; i++) w[i] = plane0[(size_t)(elt * F::W32 + i) * stride + r];
+    for (int i = 0; i < F::W32; i++) w[i] = pld(plane0 + (size_t)(elt * F::W32 + i) * stride, (uint32_t)r * 4u);
     return F::from_words(w);
 }
 template <class F>
 MH_D void pl_store(uint32_t* plane0, int elt, int stride, int r, typename F::E x) {
 #pragma unroll
-    for (int i = 0; i < F::W32; i++) plane0[(size_t)(elt * F::W32 + i) * stride + r] = F::word(x, i);
+    for (int i = 0; i < F::W32; i++) pst(plane0 + (size_t)(elt * F::W32 + i) * stride, (uint32_t)r * 4u, F::word(x, i));
 }
 
 // Field constants needed by the FLP, computed once on the host.

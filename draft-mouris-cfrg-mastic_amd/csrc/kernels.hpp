@@ -7,10 +7,11 @@
 // control flow below is wave-uniform; only data differs per lane.
 //
 // Reference mapping (poc/):
-//   k_eval_level   Vidpf.eval_with_siblings / eval_next / extend / convert /
-//                  node_proof (vidpf.py:213-380) for one tree level, plus the
-//                  per-parent payload difference of Mastic.prep_init
-//                  (mastic.py:267-271) and the truncated out shares (:311-314)
+//   k_eval_aes     Vidpf.eval_with_siblings / eval_next / extend / convert
+//                  (vidpf.py:213-364) for one tree level, plus the per-parent
+//                  payload difference of Mastic.prep_init (mastic.py:267-271)
+//                  and the truncated out shares (:311-314)
+//   k_node_proof   Vidpf.node_proof (vidpf.py:366-380) for one tree level
 //   k_absorb       the one-hot / payload binders' TurboSHAKE absorption
 //                  (mastic.py:259-287), streamed level by level
 //   k_finalize     payload/onehot checks, counter check, eval proof (:277-306)
@@ -262,58 +263,59 @@ template <> struct ConvStream<F128> {
 };
 
 // ------------------------------------------------------------- eval level
-struct LevelArgs {
+// A tree level is evaluated by two kernels:
+//   k_eval_aes    extend + correct + convert of both children of every parent
+//                 (all the AES: 2 + 2 * (1 + ceil(VL*ENC/16)) blocks per
+//                 parent), payload corrections, the parent payload difference
+//                 and the truncated out shares;
+//   k_node_proof  the children's node proofs (one Keccak-p each).
+// The next seeds and control bits of all children go through a per-level
+// plane buffer ("child seeds", 5 words per node) from the first to the second
+// kernel and to the next level's k_eval_aes.  Splitting lets the LDS-bound AES
+// run at 4 waves/SIMD and the VALU-only Keccak overlap it on another stream.
+struct AesArgs {
     int level;
-    int last_level;      // L (agg param level)
     int agg_id;
-    int n_parents;       // parents evaluated at this level (1 = the root at level 0)
+    int n_parents;       // parents at this level (1 = the root at level 0)
     int ppw;             // parents per wave
-    int path_bytes;      // ceil((level + 1) / 8)
-    int n_prefixes;
+    const int32_t* parent_node;  // [n_parents] node index of each parent in level-1 (level >= 1)
     const int32_t* child_exp;    // [2 * n_parents] index into this level's frontier, -1 = leaf
     const int32_t* child_pfx;    // [2 * n_parents] index into the prefix list (level L), -1 = none
-    const uint32_t* child_path;  // [2 * n_parents][8] MSB-first packed path words
-    // frontier planes (seed [e][4], ctrl [e], w [e][vl*w32])
-    const uint32_t* fr_seed_in;
-    const uint32_t* fr_ctrl_in;
-    const uint32_t* fr_w_in;
-    uint32_t* fr_seed_out;
-    uint32_t* fr_ctrl_out;
+    const uint32_t* cs_in;       // child seeds of level-1: [node][5]
+    uint32_t* cs_out;            // child seeds of this level: [node][5] (seed words, ctrl)
+    const uint32_t* fr_w_in;     // payloads of level-1's expanded nodes [e][vl*w32]
     uint32_t* fr_w_out;
-    uint32_t* onehot;    // [2 * n_parents * 8]   node proofs of this level (BFS order)
-    uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents
+    uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
-    PrefixState np;      // node-proof sponge prefix (kernel argument -> SGPRs)
-    const PrefixState* npp;  // the same state in device memory
 };
 
-// One workgroup = 64 reports (one per lane) x 4 waves, each wave walking its
-// own run of parents.  LDS: the replicated T-table (32 KiB), the 64 reports'
-// two AES key schedules (22 KiB, one ds_read_b128 per round) and the
-// node-proof message staging (16 KiB).
+// One workgroup = 64 reports (one per lane) x 8 waves, each wave walking its
+// own run of parents.  LDS: the replicated T-table (32 KiB) and the 64
+// reports' two AES key schedules (22 KiB, one ds_read_b128 per round) are
+// shared by all 8 waves: 54 KiB per workgroup, 2 workgroups per CU.
 template <class F>
-__global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, LevelArgs a) {
+__global__ __launch_bounds__(512) void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
     __shared__ uint32_t T[AES_LDS_WORDS];
-    __shared__ uint32_t V[16 * 256];  // node-proof message staging, [word][thread]
     __shared__ uint4 RKE[64 * 11];
     __shared__ uint4 RKC[64 * 11];
-    aes_lds_fill(T, threadIdx.x, 256);
+    aes_lds_fill(T, threadIdx.x, 512);
 
     const int S = pl.stride;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = blockIdx.x * 64 + lane;
+    const uint32_t lb = (uint32_t)r * 4u;
     {
         uint32_t* ke = (uint32_t*)RKE;
         uint32_t* kc = (uint32_t*)RKC;
-        for (int i = wave; i < 44; i += 4) {
-            ke[lane * 44 + i] = pl.rk_ext[i * S + r];
-            kc[lane * 44 + i] = pl.rk_conv[i * S + r];
+        for (int i = wave; i < 44; i += 8) {
+            ke[lane * 44 + i] = pld(pl.rk_ext + (size_t)i * S, lb);
+            kc[lane * 44 + i] = pld(pl.rk_conv + (size_t)i * S, lb);
         }
     }
     __syncthreads();
-    const int pbeg = (blockIdx.y * 4 + wave) * a.ppw;
+    const int pbeg = (blockIdx.y * 8 + wave) * a.ppw;
     if (pbeg >= a.n_parents) return;
     const int pend = min(pbeg + a.ppw, a.n_parents);
     const int l = a.level;
@@ -322,24 +324,30 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
     AesLds TL{T + (lane & 31)};
     const RkLds rke{RKE + lane * 11};
     const RkLds rkc{RKC + lane * 11};
+
     uint32_t scw[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) scw[i] = pl.cw_seed[((size_t)l * 4 + i) * S + r];
-    const uint32_t ccw = pl.cw_ctrl[(size_t)l * S + r];
+    for (int i = 0; i < 4; i++) scw[i] = pld(pl.cw_seed + ((size_t)l * 4 + i) * S, lb);
+    const uint32_t ccw = pld(pl.cw_ctrl + (size_t)l * S, lb);
     const uint32_t* wcw = pl.cw_w + (size_t)l * wl * S;
 
     for (int pi = pbeg; pi < pend; pi++) {
+        // The key schedules are re-read from LDS (one ds_read_b128 per round):
+        // without the barrier the compiler hoists all 22 reads out of the loop
+        // and pins 88 VGPRs.
+        asm volatile("" ::: "memory");
         // parent seed / control bit
         uint32_t ps[4];
         uint32_t pctrl;
         if (l == 0) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) ps[i] = pl.key[i * S + r];
+            for (int i = 0; i < 4; i++) ps[i] = pld(pl.key + (size_t)i * S, lb);
             pctrl = a.agg_id;
         } else {
+            const int pn = a.parent_node[pi];
 #pragma unroll
-            for (int i = 0; i < 4; i++) ps[i] = a.fr_seed_in[((size_t)pi * 4 + i) * S + r];
-            pctrl = a.fr_ctrl_in[(size_t)pi * S + r];
+            for (int i = 0; i < 4; i++) ps[i] = pld(a.cs_in + ((size_t)pn * 5 + i) * S, lb);
+            pctrl = pld(a.cs_in + ((size_t)pn * 5 + 4) * S, lb);
         }
         // extend: block 0 -> left child, block 1 -> right child (one paired
         // AES call), correct, then both children's convert seed blocks.
@@ -358,9 +366,17 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
             tc1 ^= (ccw >> 1) & 1u;
         }
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
+        const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            pst(a.cs_out + (n0 + i) * S, lb, ns0[i]);
+            pst(a.cs_out + (n1 + i) * S, lb, ns1[i]);
+        }
+        pst(a.cs_out + (n0 + 4) * S, lb, tc0);
+        pst(a.cs_out + (n1 + 4) * S, lb, tc1);
+
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
-
         // payloads of both children, element by element
         ConvStream<F> st0, st1;
         st0.init(cs0);
@@ -368,6 +384,7 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         const int row = 1 + p.output_len;
         for (int e = 0; e < vl; e++) {
+            asm volatile("" ::: "memory");
             st0.refill_pair(st1, TL, rkc);
             E x0 = st0.next(TL, rkc);
             E x1 = st1.next(TL, rkc);
@@ -406,42 +423,104 @@ __global__ __launch_bounds__(256) void k_eval_level(McParams p, Planes pl, Level
                 }
             }
         }
+    }
+}
 
-        // node proofs: TurboSHAKE128(seed, dst(ctx, NODE_PROOF), le16(BITS) || le16(l) || path)
-#pragma unroll 1
-        for (int c = 0; c < 2; c++) {
-            const int node = 2 * pi + c;
-            uint32_t nsc[4];
+// ------------------------------------------------------------- node proofs
+// TurboSHAKE128(seed, dst(ctx, NODE_PROOF), le16(BITS) || le16(l) || path)
+// (vidpf.py:366-380), XORed with the proof CW when the node's control bit is
+// set (vidpf.py:321-323).  The prefix le16(len(dst)) || dst || u8(16) is
+// pre-absorbed (PrefixState); the body plus the domain byte (<= 14 words)
+// lands at the uniform fill position f: a switch on f/4 selects a straight-
+// line XOR pattern, so no LDS staging and no per-lane indexing is needed.
+struct ProofArgs {
+    int level;
+    int n_nodes;
+    int npw;             // nodes per wave
+    int path_bytes;      // ceil((level + 1) / 8)
+    const uint32_t* child_path;  // [n_nodes][8]
+    const uint32_t* cs;          // child seeds of this level [node][5]
+    uint32_t* onehot;            // [n_nodes * 8]
+    const PrefixState* np;       // node-proof prefix state (device memory)
+    int f;                       // its fill position
+};
+
+#define NP_WIN 14
+template <int Q>
+MH_D void np_xor_window(KState& s, const uint32_t* x) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                nsc[i] = c ? ns1[i] : ns0[i];
-                V[i * 256 + threadIdx.x] = nsc[i];
-            }
-            V[4 * 256 + threadIdx.x] = (uint32_t)p.bits | ((uint32_t)l << 16);
-            const int pw = (a.path_bytes + 3) >> 2;
-            for (int i = 0; i < pw; i++) V[(5 + i) * 256 + threadIdx.x] = a.child_path[node * 8 + i];
-            // Re-read the (uniform) prefix state for every proof instead of
-            // pinning 50 loop-invariant registers across the parent loop.
-            asm volatile("" ::: "memory");
-            KState s = a.npp->st;
-            int f = sponge_absorb_words(s, a.np.f, 20 + a.path_bytes,
-                                        [&](int m) { return V[m * 256 + threadIdx.x]; });
-            sponge_pad(s, f, 0x01);
-            const uint32_t tcc = c ? tc1 : tc0;
-            const bool t = tcc != 0;
+    for (int k = 0; k < NP_WIN; k++)
+        if (Q + k < KECCAK_RATE_WORDS) kxor_word(s, Q + k, x[k]);
+}
+template <int Q>
+MH_D void np_xor_overflow(KState& s, const uint32_t* x) {
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                uint32_t w = kword(s, j);
-                if (t) w ^= pl.cw_proof[((size_t)l * 8 + j) * S + r];
-                a.onehot[((size_t)node * 8 + j) * S + r] = w;
-            }
-            const int ce = c ? ce1 : ce0;
-            if (ce >= 0) {
+    for (int k = 0; k < NP_WIN; k++)
+        if (Q + k >= KECCAK_RATE_WORDS) kxor_word(s, Q + k - KECCAK_RATE_WORDS, x[k]);
+}
+#define NP_CASES(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) \
+    M(15) M(16) M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) \
+    M(31) M(32) M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40) M(41)
+
+__global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, ProofArgs a) {
+    const int S = pl.stride;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = blockIdx.x * 64 + lane;
+    const uint32_t lb = (uint32_t)r * 4u;
+    const int nbeg = (blockIdx.y * 4 + wave) * a.npw;
+    if (nbeg >= a.n_nodes) return;
+    const int nend = min(nbeg + a.npw, a.n_nodes);
+    const int l = a.level;
+    uint32_t pcw[8];
 #pragma unroll
-                for (int i = 0; i < 4; i++) a.fr_seed_out[((size_t)ce * 4 + i) * S + r] = nsc[i];
-                a.fr_ctrl_out[(size_t)ce * S + r] = tcc;
+    for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)l * 8 + j) * S, lb);
+    const int f = a.f;
+    const int q = f >> 2;
+    const int sh = f & 3;
+    const int nbytes = 20 + a.path_bytes;  // body; the domain byte 0x01 follows
+    const bool cross = f + nbytes >= KECCAK_RATE;
+    const uint32_t amt = (32 - 8 * sh) & 31;
+    const int dw = nbytes >> 2;
+    const uint32_t dbit = 1u << (8 * (nbytes & 3));
+    for (int node = nbeg; node < nend; node++) {
+        // body words: seed(4) | le16(BITS) le16(l) | path (<= 8) | 0x01 | zeros
+        uint32_t B[NP_WIN];
+#pragma unroll
+        for (int i = 0; i < 4; i++) B[i] = pld(a.cs + ((size_t)node * 5 + i) * S, lb);
+        B[4] = (uint32_t)p.bits | ((uint32_t)l << 16);
+#pragma unroll
+        for (int k = 5; k < NP_WIN; k++) B[k] = k - 5 < 8 ? a.child_path[node * 8 + (k - 5)] : 0u;
+#pragma unroll
+        for (int k = 4; k < NP_WIN; k++) B[k] |= (k == dw) ? dbit : 0u;
+        const uint32_t t = pld(a.cs + ((size_t)node * 5 + 4) * S, lb);
+        // shift the window to byte position f % 4
+        uint32_t x[NP_WIN];
+#pragma unroll
+        for (int k = 0; k < NP_WIN; k++) {
+            const uint32_t hi = B[k];
+            const uint32_t lo = k ? B[k - 1] : 0u;
+            x[k] = sh ? __builtin_amdgcn_alignbit(hi, lo, amt) : hi;
+        }
+        asm volatile("" ::: "memory");  // re-read the uniform prefix state, do not pin 50 registers
+        KState s = a.np->st;
+        switch (q) {
+#define NP_W(Q) case Q: np_xor_window<Q>(s, x); break;
+            NP_CASES(NP_W)
+#undef NP_W
+        }
+        if (cross) {
+            keccak_p12(s);
+            switch (q) {
+#define NP_O(Q) case Q: np_xor_overflow<Q>(s, x); break;
+                NP_CASES(NP_O)
+#undef NP_O
             }
         }
+        s.a[20].hi ^= 0x80000000u;
+        keccak_p12(s);
+#pragma unroll
+        for (int j = 0; j < 8; j++) pst(a.onehot + ((size_t)node * 8 + j) * S, lb, kword(s, j) ^ (t ? pcw[j] : 0u));
     }
 }
 
@@ -470,10 +549,11 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     if (nb == 0) return;
     const int S = pl.stride;
     uint32_t* sp = which == 0 ? pl.sp_onehot : pl.sp_payload;
-    const uint32_t* seg = a.seg[which] + r;
+    const uint32_t* seg = a.seg[which];
+    const uint32_t lb = (uint32_t)r * 4u;
     KState s;
 #pragma unroll
-    for (int i = 0; i < 25; i++) s.a[i] = u32x2{sp[(2 * i) * S + r], sp[(2 * i + 1) * S + r]};
+    for (int i = 0; i < 25; i++) s.a[i] = u32x2{pld(sp + (size_t)(2 * i) * S, lb), pld(sp + (size_t)(2 * i + 1) * S, lb)};
     const int f = a.f[which];
     const int q = f >> 2;
     const int sh = f & 3;
@@ -486,13 +566,13 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
         if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
             const uint32_t* p = seg + (size_t)base * S;
 #pragma unroll
-            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) w[j] = p[(size_t)j * S];
+            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) w[j] = pld(p + (size_t)j * S, lb);
         } else {
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
                 const int m = base + j;
                 const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-                w[j] = seg[(size_t)mc * S];
+                w[j] = pld(seg + (size_t)mc * S, lb);
             }
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
@@ -518,8 +598,8 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 25; i++) {
-        sp[(2 * i) * S + r] = s.a[i].lo;
-        sp[(2 * i + 1) * S + r] = s.a[i].hi;
+        pst(sp + (size_t)(2 * i) * S, lb, s.a[i].lo);
+        pst(sp + (size_t)(2 * i + 1) * S, lb, s.a[i].hi);
     }
 }
 

@@ -50,7 +50,9 @@ struct Tree {
     std::vector<size_t> off;           // per-level offset into the node arrays
     std::vector<int32_t> child_exp, child_pfx;
     std::vector<uint32_t> child_path;  // 8 words per node
-    DevBuf d_exp, d_pfx, d_path;
+    std::vector<size_t> poff;          // per-level offset into parent_node
+    std::vector<int32_t> parent_node;  // node index (in level l-1) of every parent of level l
+    DevBuf d_exp, d_pfx, d_path, d_parent;
     uint64_t nodes = 0, interior = 0;
     int max_level_nodes = 0, max_exp = 0, max_parents = 0;
 };
@@ -79,6 +81,7 @@ struct mastic_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // level evals, setup, finalize, FLP
     hipStream_t stream2 = nullptr;  // binder sponges (overlap the next level's eval)
+    hipStream_t stream3 = nullptr;  // node proofs (VALU-only, overlap the LDS-bound AES)
     std::vector<hipEvent_t> sync_ev;
     PrefixState pfx_host[PFX_COUNT];
     std::string err;
@@ -92,7 +95,7 @@ struct mastic_ctx {
     Result res[2];
     // timing
     std::vector<hipEvent_t> ev;
-    double t_eval = 0, t_absorb = 0, t_total = 0;
+    double t_eval = 0, t_proof = 0, t_absorb = 0, t_total = 0;
     int n_eval = 0, n_absorb = 0;
     ~mastic_ctx() {
         for (auto& kv : trees) delete kv.second;
@@ -100,6 +103,7 @@ struct mastic_ctx {
         for (auto e : sync_ev) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (stream2) (void)hipStreamDestroy(stream2);
+        if (stream3) (void)hipStreamDestroy(stream3);
     }
 };
 
@@ -277,6 +281,14 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
             l == 0 ? std::vector<std::vector<uint8_t>>{root} : exp[l - 1];
         const int np = (int)parents.size();
         t->n_parents.push_back(np);
+        t->poff.push_back(t->parent_node.size());
+        if (l > 0) {
+            // parents of level l are level l-1's expanded nodes; find their node index
+            const size_t prev = t->off[l - 1];
+            const int prev_nodes = 2 * t->n_parents[l - 1];
+            for (int k = 0; k < prev_nodes; k++)
+                if (t->child_exp[prev + k] >= 0) t->parent_node.push_back(k);
+        }
         t->n_exp.push_back(l < level ? (int)exp[l].size() : 0);
         t->off.push_back(total);
         for (int pi = 0; pi < np; pi++) {
@@ -306,9 +318,17 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         if (l > 0) t->interior += np;
     }
     t->nodes = total;
-    if (!t->d_exp.ensure(total * 4) || !t->d_pfx.ensure(total * 4) || !t->d_path.ensure(total * 32)) {
+    const size_t npar = std::max<size_t>(t->parent_node.size(), 1);
+    if (!t->d_exp.ensure(total * 4) || !t->d_pfx.ensure(total * 4) || !t->d_path.ensure(total * 32) ||
+        !t->d_parent.ensure(npar * 4)) {
         delete t;
         return fail(c, MASTIC_ENOMEM, "out of device memory (tree)");
+    }
+    if (!t->parent_node.empty() &&
+        hipMemcpy(t->d_parent.p, t->parent_node.data(), t->parent_node.size() * 4, hipMemcpyHostToDevice) !=
+            hipSuccess) {
+        delete t;
+        return fail(c, MASTIC_EHIP, "tree upload failed");
     }
     hipError_t e1 = hipMemcpy(t->d_exp.p, t->child_exp.data(), total * 4, hipMemcpyHostToDevice);
     hipError_t e2 = hipMemcpy(t->d_pfx.p, t->child_pfx.data(), total * 4, hipMemcpyHostToDevice);
@@ -330,8 +350,8 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
 struct WorkLayout {
     size_t words = 0;  // per report (plane count)
     size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
-        rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, fr_seed[2], fr_ctrl[2],
-        fr_w[2], onehot[3], payload[3], out;
+        rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, cs[2], fr_w[2], onehot[3],
+        payload[3], out;
 };
 static constexpr int NSLOT = 3;  // level buffers in flight between eval and absorb
 
@@ -368,8 +388,7 @@ static WorkLayout work_layout(const McParams& p, const Tree* t) {
     w.verifier = take((size_t)p.verifier_len * p.w32);
     w.status = take(1);
     for (int s = 0; s < 2; s++) {
-        w.fr_seed[s] = take((size_t)std::max(t->max_exp, 1) * 4);
-        w.fr_ctrl[s] = take(std::max(t->max_exp, 1));
+        w.cs[s] = take((size_t)t->max_level_nodes * 5);
         w.fr_w[s] = take((size_t)std::max(t->max_exp, 1) * wl);
     }
     for (int k = 0; k < NSLOT; k++) {
@@ -465,57 +484,77 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const int wlw = p.value_len * p.w32;
     int f_oh = c->pfx_f[PFX_ONEHOT], f_pl = c->pfx_f[PFX_PAYLOAD];
     auto plane = [&](size_t off) { return W + off * (size_t)stride; };
-    // eval of level l+1.. runs while the binder sponges absorb level l: the
-    // sponges are serial per report (latency-bound), the evals fill the chip.
+    // Three streams per level l:
+    //   stream   k_eval_aes(l)   (LDS-bound AES, 4 waves/SIMD)
+    //   stream3  k_node_proof(l) (VALU-only Keccak) after eval_aes(l)
+    //   stream2  k_absorb(l)     (serial binder sponges) after node_proof(l)
+    // so level l+1's AES overlaps level l's proofs and sponges.  Buffers:
+    // child seeds 2 slots (aes(l) waits node_proof(l-2)), proof / payload
+    // 3 slots (aes(l), node_proof(l) wait absorb(l-3)).
     size_t sev = 0;
-    std::vector<hipEvent_t> abs_done(t->L + 1);
+    std::vector<hipEvent_t> abs_done(t->L + 1), np_done(t->L + 1);
     for (int l = 0; l <= t->L; l++) {
         const int slot = l % NSLOT;
+        const int np_ = t->n_parents[l];
+        const int nn = 2 * np_;
         if (l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
-        LevelArgs a;
+        if (l >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, np_done[l - 2], 0));
+        AesArgs a;
         a.level = l;
-        a.last_level = t->L;
         a.agg_id = agg_id;
-        a.n_parents = t->n_parents[l];
-        a.ppw = choose_ppw(a.n_parents, groups);
-        a.path_bytes = (l + 1 + 7) / 8;
-        a.n_prefixes = t->n_prefixes;
+        a.n_parents = np_;
+        a.ppw = choose_ppw(np_, groups * 2);
+        a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
-        a.child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
-        const int sin = (l + 1) & 1, sout = l & 1;
-        a.fr_seed_in = plane(wl.fr_seed[sin]);
-        a.fr_ctrl_in = plane(wl.fr_ctrl[sin]);
-        a.fr_w_in = plane(wl.fr_w[sin]);
-        a.fr_seed_out = plane(wl.fr_seed[sout]);
-        a.fr_ctrl_out = plane(wl.fr_ctrl[sout]);
-        a.fr_w_out = plane(wl.fr_w[sout]);
-        a.onehot = plane(wl.onehot[slot]);
+        a.cs_in = plane(wl.cs[(l + 1) & 1]);
+        a.cs_out = plane(wl.cs[l & 1]);
+        a.fr_w_in = plane(wl.fr_w[(l + 1) & 1]);
+        a.fr_w_out = plane(wl.fr_w[l & 1]);
         a.payload = plane(wl.payload[slot]);
         a.out = plane(wl.out);
-        a.np = c->pfx_host[PFX_NODE];
-        a.npp = (const PrefixState*)c->pfx.p + PFX_NODE;
-        dim3 grid(groups, (a.n_parents + 4 * a.ppw - 1) / (4 * a.ppw));
+        dim3 grid(groups, (np_ + 8 * a.ppw - 1) / (8 * a.ppw));
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        hipLaunchKernelGGL(k_eval_level<F>, grid, dim3(256), 0, c->stream, p, pl, a);
+        hipLaunchKernelGGL(k_eval_aes<F>, grid, dim3(512), 0, c->stream, p, pl, a);
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipGetLastError());
-        hipEvent_t ev_done = get_sync_event(c, sev++);
-        HIPCHK(c, hipEventRecord(ev_done, c->stream));
+        hipEvent_t aes_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(aes_done, c->stream));
+
+        ProofArgs pa;
+        pa.level = l;
+        pa.n_nodes = nn;
+        pa.npw = choose_ppw(nn, groups);
+        pa.path_bytes = (l + 1 + 7) / 8;
+        pa.child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
+        pa.cs = a.cs_out;
+        pa.onehot = plane(wl.onehot[slot]);
+        pa.np = (const PrefixState*)c->pfx.p + PFX_NODE;
+        pa.f = c->pfx_f[PFX_NODE];
+        HIPCHK(c, hipStreamWaitEvent(c->stream3, aes_done, 0));
+        if (l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream3, abs_done[l - NSLOT], 0));
+        hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
+        HIPCHK(c, hipEventRecord(e2, c->stream3));
+        hipLaunchKernelGGL(k_node_proof, dim3(groups, (nn + 4 * pa.npw - 1) / (4 * pa.npw)), dim3(256), 0,
+                           c->stream3, p, pl, pa);
+        HIPCHK(c, hipEventRecord(e3, c->stream3));
+        HIPCHK(c, hipGetLastError());
+        np_done[l] = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(np_done[l], c->stream3));
 
         AbsorbArgs ab;
-        ab.seg[0] = a.onehot;
-        ab.nbytes[0] = 2 * a.n_parents * 32;
+        ab.seg[0] = pa.onehot;
+        ab.nbytes[0] = nn * 32;
         ab.f[0] = f_oh;
         ab.seg[1] = a.payload;
-        ab.nbytes[1] = l > 0 ? a.n_parents * wlw * 4 : 0;
+        ab.nbytes[1] = l > 0 ? np_ * wlw * 4 : 0;
         ab.f[1] = f_pl;
-        HIPCHK(c, hipStreamWaitEvent(c->stream2, ev_done, 0));
-        hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
-        HIPCHK(c, hipEventRecord(e2, c->stream2));
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, np_done[l], 0));
+        hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
+        HIPCHK(c, hipEventRecord(e4, c->stream2));
         hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
-        HIPCHK(c, hipEventRecord(e3, c->stream2));
+        HIPCHK(c, hipEventRecord(e5, c->stream2));
         HIPCHK(c, hipGetLastError());
         abs_done[l] = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(abs_done[l], c->stream2));
@@ -730,32 +769,40 @@ extern "C" int mastic_synchronize(mastic_ctx* c) {
 
 extern "C" int mastic_last_timing(mastic_ctx* c, double* eval_ms, int* eval_launches, double* absorb_ms,
                                   int* absorb_launches, double* total_ms) {
+    return mastic_last_timing3(c, eval_ms, eval_launches, nullptr, nullptr, absorb_ms, absorb_launches, total_ms);
+}
+
+extern "C" int mastic_last_timing3(mastic_ctx* c, double* aes_ms, int* aes_launches, double* proof_ms,
+                                   int* proof_launches, double* absorb_ms, int* absorb_launches, double* total_ms) {
     if (!c) return MASTIC_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->n_eval < 0) {
+        // events: [t0, t1] then per level [aes0, aes1, proof0, proof1, absorb0, absorb1]
         const size_t evi = (size_t)(-c->n_eval);
-        double te = 0, ta = 0;
-        int ne = 0, na = 0;
+        double ta = 0, tp = 0, tb = 0;
+        int n = 0;
         float ms = 0;
-        // events: [t0, t1] then per level [e0, e1, e2, e3]
-        for (size_t i = 2; i + 3 < evi + 1 && i + 3 <= evi - 1 + 1; i += 4) {
-            if (i + 3 >= evi) break;
+        for (size_t i = 2; i + 6 <= evi; i += 6) {
             HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
-            te += ms;
-            ne++;
-            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i + 2], c->ev[i + 3]));
             ta += ms;
-            na++;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i + 2], c->ev[i + 3]));
+            tp += ms;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i + 4], c->ev[i + 5]));
+            tb += ms;
+            n++;
         }
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
         c->t_total = ms;
-        c->t_eval = te;
-        c->t_absorb = ta;
-        c->n_eval = ne;
-        c->n_absorb = na;
+        c->t_eval = ta;
+        c->t_proof = tp;
+        c->t_absorb = tb;
+        c->n_eval = n;
+        c->n_absorb = n;
     }
-    if (eval_ms) *eval_ms = c->t_eval;
-    if (eval_launches) *eval_launches = c->n_eval;
+    if (aes_ms) *aes_ms = c->t_eval;
+    if (aes_launches) *aes_launches = c->n_eval;
+    if (proof_ms) *proof_ms = c->t_proof;
+    if (proof_launches) *proof_launches = c->n_absorb;
     if (absorb_ms) *absorb_ms = c->t_absorb;
     if (absorb_launches) *absorb_launches = c->n_absorb;
     if (total_ms) *total_ms = c->t_total;
@@ -1008,7 +1055,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->p = p;
     c->device = up->device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MASTIC_EHIP;
     }

@@ -27,7 +27,7 @@ EXPORTS = [
     "mastic_reports_shard", "mastic_prep_init", "mastic_prep_result", "mastic_aggregate",
     "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
     "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
-    "mastic_work_bytes",
+    "mastic_work_bytes", "mastic_last_timing3",
 ]
 
 
@@ -116,6 +116,8 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
                     "mastic_fold_shares": (i32, [P, P, sz, sz, P]),
+                    "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3
+                                            + [ctypes.POINTER(ctypes.c_double)]),
                     "mastic_work_bytes": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64)]),
                     "mastic_tree_stats": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64),
                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),

@@ -243,6 +243,15 @@ class Mastic:
                                                         ctypes.byref(a), ctypes.byref(na), ctypes.byref(t)))
         return (e.value, ne.value, a.value, na.value, t.value)
 
+    def last_timing3(self):
+        """(aes_ms, aes_launches, proof_ms, proof_launches, absorb_ms, absorb_launches, total_ms)."""
+        v = [ctypes.c_double() for _ in range(4)]
+        k = [ctypes.c_int() for _ in range(3)]
+        _check(self._ctx, _lib.lib().mastic_last_timing3(
+            self._ctx, ctypes.byref(v[0]), ctypes.byref(k[0]), ctypes.byref(v[1]), ctypes.byref(k[1]),
+            ctypes.byref(v[2]), ctypes.byref(k[2]), ctypes.byref(v[3])))
+        return (v[0].value, k[0].value, v[1].value, k[1].value, v[2].value, k[2].value, v[3].value)
+
     def tree_stats(self, agg_param):
         enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()

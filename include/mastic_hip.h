@@ -159,14 +159,18 @@ int mastic_shard_batch(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_len, 
                        uint8_t* input_shares0_out, uint8_t* input_shares1_out);
 
 /* ---- measurement hooks (bench) --------------------------------------- */
-/* Device time (ms) of the VIDPF level-eval kernels and of the binder-absorb
- * kernels during the last prep_init, measured with HIP events on the ctx's
- * stream; also their launch counts. */
+/* Device time (ms) of the VIDPF level-eval (AES) kernels and of the
+ * binder-absorb kernels during the last prep_init, measured with HIP events on
+ * the streams the kernels run on; also their launch counts. */
 int mastic_last_timing(mastic_ctx* ctx, double* eval_ms, int* eval_launches, double* absorb_ms,
                        int* absorb_launches, double* total_ms);
 /* HBM work-buffer bytes one report needs during prep_init with this agg
  * param (prep_init processes reports in chunks of budget / this). */
 int mastic_work_bytes(mastic_ctx* ctx, const uint8_t* enc_agg_param, size_t agg_param_len, uint64_t* per_report);
+/* The same split three ways: VIDPF AES level kernels, node-proof (Keccak)
+ * level kernels, binder-sponge kernels (ms summed over launches). */
+int mastic_last_timing3(mastic_ctx* ctx, double* aes_ms, int* aes_launches, double* proof_ms, int* proof_launches,
+                        double* absorb_ms, int* absorb_launches, double* total_ms);
 /* Tree statistics of an encoded agg param: nodes evaluated per report,
  * interior nodes, max nodes on one level. */
 int mastic_tree_stats(mastic_ctx* ctx, const uint8_t* enc_agg_param, size_t agg_param_len, uint64_t* nodes,
