@@ -1,0 +1,110 @@
+"""Weighted heavy-hitters level sweep.
+
+Mirrors the reference driver ``compute_heavy_hitters`` (poc/examples.py:37-91)
+and ``get_threshold`` (poc/examples.py:26-34): walk the prefix tree level by
+level, keep the children of every candidate whose aggregate reaches its
+threshold, report the surviving full-length prefixes.
+
+Differences from the reference loop, all in how the work is batched, not in
+what is computed:
+  * the reports are uploaded to HBM once and every level runs as one batched
+    ``prep_init`` per aggregator (GPU), one ``decide_batch`` and one GPU fold
+    per aggregator, instead of a Python loop over reports;
+  * a report that fails verification at some level (the reference would raise
+    at ``prep_shares_to_prep``) is dropped from that level's aggregate and
+    from every later level, which is what a deployed aggregator does.  With
+    only honest reports the output is identical to the reference's.
+"""
+import numpy as np
+
+from .vdaf import Mastic
+
+
+def get_threshold(thresholds, prefix):
+    """poc/examples.py:26-34: the threshold of the longest proper prefix of
+    ``prefix`` listed in ``thresholds`` (the prefix itself excluded), else
+    ``thresholds['default']``."""
+    for level in reversed(range(len(prefix) - 1)):
+        if prefix[:level + 1] in thresholds:
+            return thresholds[prefix[:level + 1]]
+    return thresholds['default']
+
+
+def _encode_reports(mastic: Mastic, reports):
+    nonces = b"".join(r[0] for r in reports)
+    pubs = b"".join(mastic.encode_public_share(r[1]) for r in reports)
+    in0 = b"".join(mastic.test_vec_encode_input_share(r[2][0]) for r in reports)
+    in1 = b"".join(mastic.test_vec_encode_input_share(r[2][1]) for r in reports)
+    return (nonces, pubs, in0, in1)
+
+
+class SweepLevel:
+    """What one level of the sweep did (for callers that want the trace)."""
+
+    def __init__(self, level, prefixes, agg_result, n_valid):
+        self.level = level
+        self.prefixes = prefixes
+        self.agg_result = agg_result
+        self.n_valid = n_valid
+
+
+def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verify_key: bytes = None,
+                          trace=None):
+    """poc/examples.py:37-91 on the GPU.
+
+    ``reports`` is either the reference's list of
+    ``(nonce, public_share, input_shares)`` tuples or a device-resident
+    :class:`~mastic_amd.vdaf.Reports` batch holding both input shares
+    (``Mastic.reports_shard`` / ``reports_upload``).  ``verify_key`` defaults
+    to fresh randomness, as in the reference.  If ``trace`` is a list, one
+    :class:`SweepLevel` per level is appended to it.
+    """
+    if verify_key is None:
+        import os
+        verify_key = os.urandom(mastic.VERIFY_KEY_SIZE)
+    if isinstance(reports, (list, tuple)):
+        if len(reports) == 0:
+            dev = None
+        else:
+            dev = mastic.reports_upload(*_encode_reports(mastic, reports))
+    else:
+        dev = reports
+    n = 0 if dev is None else dev.n
+    alive = np.ones(n, dtype=bool)
+
+    prefixes = [(False,), (True,)]
+    prev_agg_params = []
+    heavy_hitters = []
+    bits = mastic.vidpf.BITS
+    for level in range(bits):
+        agg_param = (level, tuple(prefixes), level == 0)
+        assert mastic.is_valid(agg_param, prev_agg_params)
+
+        if n and prefixes:
+            shares = []
+            for agg_id in range(2):
+                mastic.prep_init_device(dev, verify_key, ctx, agg_id, agg_param)
+                shares.append(mastic.prep_result(dev, agg_id, agg_param))
+            (_msgs, valid) = mastic.decide_batch(ctx, agg_param, shares[0][0], shares[1][0])
+            alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
+            mask = alive.astype(np.uint8)
+            agg_shares = [mastic.aggregate_device(agg_id, agg_param, mask) for agg_id in range(2)]
+        else:
+            agg_shares = [mastic.agg_init(agg_param) for _ in range(2)]
+        agg_result = mastic.unshard(agg_param, agg_shares, int(alive.sum()))
+        prev_agg_params.append(agg_param)
+        if trace is not None:
+            trace.append(SweepLevel(level, list(prefixes), agg_result, int(alive.sum())))
+
+        if level < bits - 1:
+            next_prefixes = []
+            for (prefix, count) in zip(prefixes, agg_result):
+                if count >= get_threshold(thresholds, prefix):
+                    next_prefixes.append(prefix + (False,))
+                    next_prefixes.append(prefix + (True,))
+            prefixes = next_prefixes
+        else:
+            for (prefix, count) in zip(prefixes, agg_result):
+                if count >= get_threshold(thresholds, prefix):
+                    heavy_hitters.append(prefix)
+    return heavy_hitters

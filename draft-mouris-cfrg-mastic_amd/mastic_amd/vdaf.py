@@ -44,6 +44,30 @@ def _pack_bits_lsb(bits) -> bytes:
     return bytes(out)
 
 
+class VidpfInfo:
+    """The parts of ``poc/vidpf.py``'s ``Vidpf`` object that drivers read
+    through ``mastic.vidpf`` (constants :85-100, index helpers :418-427); the
+    VIDPF itself runs in the HIP kernels."""
+
+    KEY_SIZE = 16
+    NONCE_SIZE = 16
+    RAND_SIZE = 32
+
+    def __init__(self, field, bits: int, value_len: int):
+        self.field = field
+        self.BITS = bits
+        self.VALUE_LEN = value_len
+
+    def test_index_from_int(self, value: int, length: int):
+        """poc/vidpf.py:418-422 (MSB first)."""
+        assert length <= self.BITS
+        return tuple((value >> (length - 1 - i)) & 1 != 0 for i in range(length))
+
+    def prefixes_for_level(self, level: int):
+        """poc/vidpf.py:424-427"""
+        return tuple(self.test_index_from_int(value, level + 1) for value in range(2 ** level))
+
+
 class Mastic:
     """Mastic(bits, valid) with the validity circuit given as (name, params)."""
 
@@ -81,6 +105,7 @@ class Mastic:
         self.sum_vec_bits = sum_vec_bits
         self.max_measurement = max_measurement
         self.chunk_length = chunk_length
+        self.vidpf = VidpfInfo(self.field, bits, sz.value_len)
         if circuit == "Sum":
             self._wbits = max_measurement.bit_length()
             self._offset = 2 ** self._wbits - 1 - max_measurement
@@ -231,6 +256,21 @@ class Mastic:
         enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
         _check(self._ctx, _lib.lib().mastic_prep_init(self._ctx, reports._ptr, verify_key, ctx, len(ctx), agg_id,
                                                       enc, len(enc)))
+
+    def prep_result(self, reports, agg_id: int, agg_param, want_out_shares=False):
+        """Wire results of the last prep_init_device for agg_id:
+        (prep_shares bytes, jr_seeds bytes, out_shares bytes or None, status int32 array)."""
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        (_level, count, wc) = self._agg_param_header(enc)
+        n = reports.n
+        ps = np.empty(n * self.prep_share_size(wc), np.uint8)
+        js = np.empty(n * 32, np.uint8)
+        out = np.empty(n * count * (1 + self.OUTPUT_LEN) * self.field.ENCODED_SIZE, np.uint8) \
+            if want_out_shares else None
+        st = np.empty(n, np.int32)
+        _check(self._ctx, _lib.lib().mastic_prep_result(self._ctx, agg_id, _lib.buf(ps), _lib.buf(js),
+                                                        _lib.buf(out), _lib.buf(st)))
+        return (ps.tobytes(), js.tobytes(), None if out is None else out.tobytes(), st)
 
     def synchronize(self):
         _check(self._ctx, _lib.lib().mastic_synchronize(self._ctx))
