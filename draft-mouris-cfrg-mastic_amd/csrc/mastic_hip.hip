@@ -90,6 +90,7 @@ struct mastic_ctx {
     DevBuf pfx;      // PrefixState[PFX_COUNT]
     DevBuf pfx_bytes, pfx_meta;
     DevBuf consts;   // alpha^-i table for prove
+    DevBuf agg_valid, agg_out;  // mastic_aggregate staging
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
@@ -106,6 +107,21 @@ struct mastic_ctx {
         if (stream3) (void)hipStreamDestroy(stream3);
     }
 };
+
+// Every entry point that touches the GPU runs with the ctx's device current
+// (and restores the caller's), so contexts on different GPUs can be driven
+// from one thread.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(const mastic_ctx* c);
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+DeviceScope::DeviceScope(const mastic_ctx* c) {
+    int cur = -1;
+    if (c && hipGetDevice(&cur) == hipSuccess && cur != c->device && hipSetDevice(c->device) == hipSuccess) prev = cur;
+}
 
 static int fail(mastic_ctx* c, int code, const char* fmt, ...) {
     if (c) {
@@ -338,6 +354,7 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         return fail(c, MASTIC_EHIP, "tree upload failed");
     }
     if (c->trees.size() > 64) {
+        (void)hipDeviceSynchronize();  // cached trees may still be read by queued kernels
         for (auto& kv : c->trees) delete kv.second;
         c->trees.clear();
     }
@@ -598,6 +615,7 @@ static uint64_t default_budget(mastic_ctx* c) {
 extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_t verify_key[32],
                                 const uint8_t* app_ctx, size_t ctx_len, int agg_id, const uint8_t* enc_agg_param,
                                 size_t agg_param_len) {
+    DeviceScope ds_(c);
     if (!c || !rep || rep->ctx != c) return fail(c, MASTIC_EINVAL, "bad ctx/reports");
     if (agg_id != 0 && agg_id != 1) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     if ((agg_id == 0 && !rep->in0.p) || (agg_id == 1 && !rep->in1.p))
@@ -670,6 +688,7 @@ static int fetch(mastic_ctx* c, const DevBuf& b, size_t planes, size_t stride, s
 
 extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_shares, uint8_t* jr_seeds,
                                   uint8_t* out_shares, int32_t* status) {
+    DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     Result& R = c->res[agg_id];
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
@@ -717,12 +736,14 @@ extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_share
 }
 
 extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid, uint8_t* agg_share) {
+    DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     Result& R = c->res[agg_id];
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
     const McParams& p = c->p;
     const size_t rows = (size_t)R.n_prefixes * (1 + p.output_len);
-    static thread_local DevBuf dvalid, dagg;
+    DevBuf& dvalid = c->agg_valid;
+    DevBuf& dagg = c->agg_out;
     const uint8_t* dv = nullptr;
     if (valid && R.n) {
         if (!dvalid.ensure(R.n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
@@ -746,6 +767,7 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
 
 extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t n_shares, size_t n_elems,
                                   void* dev_out) {
+    DeviceScope ds_(c);
     if (!c || (!dev_shares && n_shares) || !dev_out) return MASTIC_EINVAL;
     if (n_elems == 0) return 0;
     HIPCHK(c, hipDeviceSynchronize());  // the shares may come from another stream (RCCL)
@@ -762,6 +784,7 @@ extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t 
 }
 
 extern "C" int mastic_synchronize(mastic_ctx* c) {
+    DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
@@ -774,6 +797,7 @@ extern "C" int mastic_last_timing(mastic_ctx* c, double* eval_ms, int* eval_laun
 
 extern "C" int mastic_last_timing3(mastic_ctx* c, double* aes_ms, int* aes_launches, double* proof_ms,
                                    int* proof_launches, double* absorb_ms, int* absorb_launches, double* total_ms) {
+    DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->n_eval < 0) {
@@ -811,6 +835,7 @@ extern "C" int mastic_last_timing3(mastic_ctx* c, double* aes_ms, int* aes_launc
 
 extern "C" int mastic_tree_stats(mastic_ctx* c, const uint8_t* enc, size_t len, uint64_t* nodes, uint64_t* interior,
                                  uint64_t* max_level_nodes) {
+    DeviceScope ds_(c);
     Tree* t = nullptr;
     int rc = build_tree(c, enc, len, &t);
     if (rc) return rc;
@@ -821,6 +846,7 @@ extern "C" int mastic_tree_stats(mastic_ctx* c, const uint8_t* enc, size_t len, 
 }
 
 extern "C" int mastic_work_bytes(mastic_ctx* c, const uint8_t* enc, size_t len, uint64_t* per_report) {
+    DeviceScope ds_(c);
     Tree* t = nullptr;
     int rc = build_tree(c, enc, len, &t);
     if (rc) return rc;
@@ -833,6 +859,7 @@ extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t verify_key[32
                                       size_t n, const uint8_t* nonces, const uint8_t* public_shares,
                                       const uint8_t* input_shares, uint8_t* prep_shares_out, uint8_t* jr_seeds_out,
                                       uint8_t* out_shares_out, int32_t* status_out) {
+    DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     if (agg_id != 0 && agg_id != 1) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     mastic_reports* rep = nullptr;
@@ -850,6 +877,7 @@ extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t verify_key[32
 extern "C" int mastic_decide_batch(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* enc,
                                    size_t len, size_t n, const uint8_t* ps0, const uint8_t* ps1, uint8_t* msgs_out,
                                    uint8_t* valid_out) {
+    DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     Tree* t = nullptr;
     int rc = build_tree(c, enc, len, &t);
@@ -884,6 +912,7 @@ extern "C" int mastic_decide_batch(mastic_ctx* c, const uint8_t* app_ctx, size_t
 
 // ---------------------------------------------------------------- reports
 extern "C" int mastic_reports_create(mastic_ctx* c, size_t n, mastic_reports** out) {
+    DeviceScope ds_(c);
     if (!c || !out) return MASTIC_EINVAL;
     mastic_reports* r = new mastic_reports();
     r->ctx = c;
@@ -897,11 +926,15 @@ extern "C" int mastic_reports_create(mastic_ctx* c, size_t n, mastic_reports** o
     return 0;
 }
 
-extern "C" void mastic_reports_destroy(mastic_reports* r) { delete r; }
+extern "C" void mastic_reports_destroy(mastic_reports* r) {
+    DeviceScope ds_(r ? r->ctx : nullptr);
+    delete r;
+}
 extern "C" size_t mastic_reports_count(const mastic_reports* r) { return r ? r->n : 0; }
 
 extern "C" int mastic_reports_upload(mastic_reports* r, const uint8_t* nonces, const uint8_t* pub,
                                      const uint8_t* in0, const uint8_t* in1) {
+    DeviceScope ds_(r ? r->ctx : nullptr);
     if (!r) return MASTIC_EINVAL;
     mastic_ctx* c = r->ctx;
     const McParams& p = c->p;
@@ -920,6 +953,7 @@ extern "C" int mastic_reports_upload(mastic_reports* r, const uint8_t* nonces, c
 }
 
 extern "C" int mastic_reports_download(mastic_reports* r, uint8_t* nonces, uint8_t* pub, uint8_t* in0, uint8_t* in1) {
+    DeviceScope ds_(r ? r->ctx : nullptr);
     if (!r) return MASTIC_EINVAL;
     mastic_ctx* c = r->ctx;
     const McParams& p = c->p;
@@ -1012,6 +1046,7 @@ static int shard_impl(mastic_ctx* c, mastic_reports* rep, const uint8_t* alphas,
 extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx, size_t ctx_len,
                                     const uint8_t* alphas, const uint8_t* betas, const uint8_t* nonces,
                                     const uint8_t* rands) {
+    DeviceScope ds_(rep ? rep->ctx : nullptr);
     if (!rep) return MASTIC_EINVAL;
     mastic_ctx* c = rep->ctx;
     if (rep->n == 0) return 0;
@@ -1025,6 +1060,7 @@ extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx,
 extern "C" int mastic_shard_batch(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, size_t n,
                                   const uint8_t* alphas, const uint8_t* betas, const uint8_t* nonces,
                                   const uint8_t* rands, uint8_t* pub_out, uint8_t* in0_out, uint8_t* in1_out) {
+    DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     mastic_reports* rep = nullptr;
     int rc = mastic_reports_create(c, n, &rep);
@@ -1065,8 +1101,11 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
 }
 
 extern "C" void mastic_ctx_destroy(mastic_ctx* c) {
+    DeviceScope ds_(c);
     if (!c) return;
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamSynchronize(c->stream3);
     delete c;
 }
 
