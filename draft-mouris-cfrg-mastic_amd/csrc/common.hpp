@@ -52,3 +52,9 @@ MH_D uint32_t pld(const uint32_t* p, uint32_t lane_bytes) {
 MH_D void pst(uint32_t* p, uint32_t lane_bytes, uint32_t v) {
     __builtin_amdgcn_raw_buffer_store_b32(v, mh_rsrc(p), lane_bytes, 0, 0);
 }
+// Word `soff / 4` of a block of planes: one descriptor per block (rs, uniform)
+// and the uniform plane offset in soffset, so a 43-plane block costs 4 SGPRs
+// for the descriptor instead of one descriptor per plane.
+MH_D uint32_t pld_so(__amdgpu_buffer_rsrc_t rs, uint32_t lane_bytes, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, lane_bytes, soff, 0);
+}

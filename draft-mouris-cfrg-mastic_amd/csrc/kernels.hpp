@@ -561,12 +561,21 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     const int amt = (32 - 8 * sh) & 31;  // block word j = alignbit(w[j+1], w[j], amt)
     const int nw = (nb + 3) >> 2;
     const int end = f + nb;
+    const uint32_t pstride = (uint32_t)S * 4u;
     auto load_block = [&](int b, uint32_t* w) {
         const int base = KECCAK_RATE_WORDS * b - q - off;
         if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
-            const uint32_t* p = seg + (size_t)base * S;
+            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * S);
+            // the plane offset is a running SGPR sum made opaque at every step,
+            // so the compiler cannot hoist 43 loop-invariant offsets (which it
+            // would spill to VGPRs and then waterfall)
+            uint32_t so = 0;
 #pragma unroll
-            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) w[j] = pld(p + (size_t)j * S, lb);
+            for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
+                w[j] = pld_so(rs, lb, so);
+                so += pstride;
+                asm volatile("" : "+s"(so));
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
@@ -601,6 +610,85 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
         pst(sp + (size_t)(2 * i) * S, lb, s.a[i].lo);
         pst(sp + (size_t)(2 * i + 1) * S, lb, s.a[i].hi);
     }
+}
+
+// Two lanes per sponge (keccak_p12_pair): lane h of report r holds state
+// words 2i + h.  Block word j = alignbit(w[j+1], w[j], amt) as above; lane h
+// needs the j = 2i + h, i.e. stream words base + h + k, k < 42, which it loads
+// itself (the plane offset h*S is part of its per-lane buffer offset).
+__global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
+    __builtin_amdgcn_s_setprio(3);
+    const int h = threadIdx.x & 1;
+    const int r = blockIdx.x * 128 + (threadIdx.x >> 1);
+    const int which = blockIdx.y;
+    if (r >= pl.stride) return;  // both lanes of a pair leave together
+    const int nb = a.nbytes[which];
+    if (nb == 0) return;
+    const int S = pl.stride;
+    uint32_t* sp = which == 0 ? pl.sp_onehot : pl.sp_payload;
+    const uint32_t* seg = a.seg[which];
+    const uint32_t lb = (uint32_t)r * 4u;
+    const uint32_t lbh = ((uint32_t)h * (uint32_t)S + (uint32_t)r) * 4u;  // plane h of the pair
+    KHalf s;
+#pragma unroll
+    for (int i = 0; i < 25; i++) s.a[i] = pld(sp + (size_t)(2 * i) * S, lbh);
+    const int f = a.f[which];
+    const int q = f >> 2;
+    const int sh = f & 3;
+    const int off = sh ? 1 : 0;
+    const int amt = (32 - 8 * sh) & 31;
+    const int nw = (nb + 3) >> 2;
+    const int end = f + nb;
+    constexpr int NL = KECCAK_RATE_WORDS;  // words loaded per lane and block
+    const uint32_t pstride = (uint32_t)S * 4u;
+    auto load_block = [&](int b, uint32_t* w) {
+        const int base = KECCAK_RATE_WORDS * b - q - off;
+        if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
+            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * S);
+            uint32_t so = 0;  // running opaque plane offset, as in k_absorb
+#pragma unroll
+            for (int k = 0; k < NL; k++) {
+                w[k] = pld_so(rs, lbh, so);
+                so += pstride;
+                asm volatile("" : "+s"(so));
+            }
+        } else {
+            // first / last block of the launch: uniform clamped loads of
+            // words base .. base + 42, zero outside [0, nw), then lane h
+            // keeps words h .. h + 41
+            uint32_t t[NL + 1];
+#pragma unroll
+            for (int k = 0; k < NL + 1; k++) {
+                const int m = base + k;
+                const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
+                t[k] = pld(seg + (size_t)mc * S, lb);
+            }
+#pragma unroll
+            for (int k = 0; k < NL + 1; k++) {
+                const int m = base + k;
+                t[k] = (m >= 0 && m < nw) ? t[k] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < NL; k++) w[k] = h ? t[k + 1] : t[k];
+        }
+    };
+    uint32_t cur[NL];
+    load_block(0, cur);
+    for (int b = 0;; b++) {
+        const bool full = end >= KECCAK_RATE * (b + 1);
+        const bool more = end > KECCAK_RATE * (b + 1);
+        uint32_t nxt[NL];
+        if (more) load_block(b + 1, nxt);
+#pragma unroll
+        for (int i = 0; i < 21; i++) s.a[i] ^= __builtin_amdgcn_alignbit(cur[2 * i + 1], cur[2 * i], amt);
+        if (!full) break;
+        keccak_p12_pair(s, h != 0);
+        if (!more) break;
+#pragma unroll
+        for (int k = 0; k < NL; k++) cur[k] = nxt[k];
+    }
+#pragma unroll
+    for (int i = 0; i < 25; i++) pst(sp + (size_t)(2 * i) * S, lbh, s.a[i]);
 }
 
 // ------------------------------------------------------------- finalize

@@ -91,6 +91,7 @@ struct mastic_ctx {
     DevBuf pfx_bytes, pfx_meta;
     DevBuf consts;   // alpha^-i table for prove
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
+    bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
@@ -570,7 +571,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipStreamWaitEvent(c->stream2, np_done[l], 0));
         hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e4, c->stream2));
-        hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
+        if (c->absorb_pair)
+            hipLaunchKernelGGL(k_absorb_pair, dim3((stride + 127) / 128, 2), dim3(256), 0, c->stream2, pl, ab);
+        else
+            hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
         HIPCHK(c, hipEventRecord(e5, c->stream2));
         HIPCHK(c, hipGetLastError());
         abs_done[l] = get_sync_event(c, sev++);
@@ -1090,6 +1094,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->user = *up;
     c->p = p;
     c->device = up->device;
+    {
+        const char* e = getenv("MASTIC_ABSORB_SINGLE");
+        c->absorb_pair = !(e && e[0] == '1');
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
