@@ -124,8 +124,8 @@ MH_D void aes128_expand(const AesLds& T, const uint32_t key[4], uint32_t rk[44])
 
 // XofFixedKeyAes128.hash_block for counter `ctr` (< 2^32 here):
 //   x = seed ^ le128(ctr); sigma(x) = x_hi || (x_hi ^ x_lo); out = AES(sigma) ^ sigma
-template <class RK>
-MH_D void fixed_key_block(const AesLds& T, const RK& rk, const uint32_t seed[4], uint32_t ctr, uint32_t out[4]) {
+template <class TT, class RK>
+MH_D void fixed_key_block(const TT& T, const RK& rk, const uint32_t seed[4], uint32_t ctr, uint32_t out[4]) {
     uint32_t x0 = seed[0] ^ ctr, x1 = seed[1], x2 = seed[2], x3 = seed[3];
     uint32_t sg[4] = {x2, x3, x2 ^ x0, x3 ^ x1};
     uint32_t c[4] = {sg[0], sg[1], sg[2], sg[3]};
@@ -183,8 +183,8 @@ MH_D void aes128_encrypt2(const AesLds& T, const RK& rk, uint32_t a[4], uint32_t
 }
 
 // Two fixed-key blocks (seed_a, ctr_a) and (seed_b, ctr_b) in lockstep.
-template <class RK>
-MH_D void fixed_key_block2(const AesLds& T, const RK& rk, const uint32_t sa[4], uint32_t ca, const uint32_t sb_[4],
+template <class TT, class RK>
+MH_D void fixed_key_block2(const TT& T, const RK& rk, const uint32_t sa[4], uint32_t ca, const uint32_t sb_[4],
                            uint32_t cb, uint32_t oa[4], uint32_t ob[4]) {
     uint32_t ga[4] = {sa[2], sa[3], sa[2] ^ sa[0] ^ ca, sa[3] ^ sa[1]};
     uint32_t gb[4] = {sb_[2], sb_[3], sb_[2] ^ sb_[0] ^ cb, sb_[3] ^ sb_[1]};
@@ -196,4 +196,99 @@ MH_D void fixed_key_block2(const AesLds& T, const RK& rk, const uint32_t sa[4], 
         oa[i] = xa[i] ^ ga[i];
         ob[i] = xb[i] ^ gb[i];
     }
+}
+
+// ---- T0/T2 table addressed by v_perm_b32 (level-eval kernel) ---------------
+// Layout (64 KiB): row x (256 B) holds T0[x] replicated at bytes 4l (lane
+// l < 32) and T2[x] = rot16(T0[x]) replicated at bytes 128 + 4l.  The LDS
+// byte address of a lookup is then  (x << 8) | lane_byte,  built from the
+// state word by ONE v_perm_b32 (byte k of the state word into bits 8..15, the
+// lane's byte into bits 0..7) instead of a bit-field extract plus a
+// shift-add.  Banks stay conflict-free: lane l always reads bank l mod 32.
+// With T2 stored, a column needs one rotation instead of three:
+//   T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = T0[a] ^ T2[c] ^ rot8(T0[b] ^ T2[d]).
+// A round costs 16 v_perm + 4 x (xor, rot, xor3, xor) = 32 VALU against
+// 52 with one rotated table and two-instruction addressing.
+#define AES_PERM_LDS_WORDS (256 * 64)
+
+MH_D void aes_perm_fill(uint32_t* T, int tid, int nthreads) {
+    for (int i = tid; i < AES_PERM_LDS_WORDS; i += nthreads) {
+        const uint32_t t0 = aes_t0(i >> 6);
+        T[i] = (i & 32) ? rot16(t0) : t0;
+    }
+}
+
+struct AesPerm {
+    const uint32_t* T;  // the 64 KiB table
+    uint32_t lb0;       // 4 * (lane & 31)
+    uint32_t lb2;       // 128 + 4 * (lane & 31)
+    template <int K>
+    MH_D uint32_t t0(uint32_t x) const {
+        const uint32_t a = __builtin_amdgcn_perm(x, lb0, 0x0c0c0000u | ((4u + K) << 8));
+        return *(const uint32_t*)((const char*)T + a);
+    }
+    template <int K>
+    MH_D uint32_t t2(uint32_t x) const {
+        const uint32_t a = __builtin_amdgcn_perm(x, lb2, 0x0c0c0000u | ((4u + K) << 8));
+        return *(const uint32_t*)((const char*)T + a);
+    }
+};
+
+// One full round column: T0[b0(w0)] ^ T1[b1(w1)] ^ T2[b2(w2)] ^ T3[b3(w3)] ^ k
+MH_D uint32_t aes_col(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t k) {
+    const uint32_t r = rot8(T.t0<1>(w1) ^ T.t2<3>(w3));
+    return xor3_u32(T.t0<0>(w0), T.t2<2>(w2), r) ^ k;
+}
+// Final-round column: S-box bytes (byte 1 of the T0 entries) packed with two
+// v_perm_b32 and merged with the round key by one xor3.
+MH_D uint32_t aes_col_last(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t k) {
+    const uint32_t lo = __builtin_amdgcn_perm(T.t0<1>(w1), T.t0<0>(w0), 0x0c0c0501u);
+    const uint32_t hi = __builtin_amdgcn_perm(T.t0<3>(w3), T.t0<2>(w2), 0x05010c0cu);
+    return xor3_u32(lo, hi, k);
+}
+
+template <class RK>
+MH_D void aes128_encrypt2(const AesPerm& T, const RK& rk, uint32_t a[4], uint32_t b[4]) {
+    uint4 k = rk(0);
+    uint32_t a0 = a[0] ^ k.x, a1 = a[1] ^ k.y, a2 = a[2] ^ k.z, a3 = a[3] ^ k.w;
+    uint32_t c0 = b[0] ^ k.x, c1 = b[1] ^ k.y, c2 = b[2] ^ k.z, c3 = b[3] ^ k.w;
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k = rk(r);
+        const uint32_t t0 = aes_col(T, a0, a1, a2, a3, k.x), u0 = aes_col(T, c0, c1, c2, c3, k.x);
+        const uint32_t t1 = aes_col(T, a1, a2, a3, a0, k.y), u1 = aes_col(T, c1, c2, c3, c0, k.y);
+        const uint32_t t2 = aes_col(T, a2, a3, a0, a1, k.z), u2 = aes_col(T, c2, c3, c0, c1, k.z);
+        const uint32_t t3 = aes_col(T, a3, a0, a1, a2, k.w), u3 = aes_col(T, c3, c0, c1, c2, k.w);
+        a0 = t0; a1 = t1; a2 = t2; a3 = t3;
+        c0 = u0; c1 = u1; c2 = u2; c3 = u3;
+    }
+    k = rk(10);
+    a[0] = aes_col_last(T, a0, a1, a2, a3, k.x);
+    b[0] = aes_col_last(T, c0, c1, c2, c3, k.x);
+    a[1] = aes_col_last(T, a1, a2, a3, a0, k.y);
+    b[1] = aes_col_last(T, c1, c2, c3, c0, k.y);
+    a[2] = aes_col_last(T, a2, a3, a0, a1, k.z);
+    b[2] = aes_col_last(T, c2, c3, c0, c1, k.z);
+    a[3] = aes_col_last(T, a3, a0, a1, a2, k.w);
+    b[3] = aes_col_last(T, c3, c0, c1, c2, k.w);
+}
+
+template <class RK>
+MH_D void aes128_encrypt(const AesPerm& T, const RK& rk, uint32_t s[4]) {
+    uint4 k = rk(0);
+    uint32_t s0 = s[0] ^ k.x, s1 = s[1] ^ k.y, s2 = s[2] ^ k.z, s3 = s[3] ^ k.w;
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k = rk(r);
+        const uint32_t t0 = aes_col(T, s0, s1, s2, s3, k.x);
+        const uint32_t t1 = aes_col(T, s1, s2, s3, s0, k.y);
+        const uint32_t t2 = aes_col(T, s2, s3, s0, s1, k.z);
+        const uint32_t t3 = aes_col(T, s3, s0, s1, s2, k.w);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    k = rk(10);
+    s[0] = aes_col_last(T, s0, s1, s2, s3, k.x);
+    s[1] = aes_col_last(T, s1, s2, s3, s0, k.y);
+    s[2] = aes_col_last(T, s2, s3, s0, s1, k.z);
+    s[3] = aes_col_last(T, s3, s0, s1, s2, k.w);
 }

@@ -201,8 +201,8 @@ template <> struct ConvStream<F64> {
     }
     // Common case: both children's streams need their next block at the same
     // element (no rejection so far): produce both in one paired AES call.
-    template <class RK>
-    MH_D void refill_pair(ConvStream& o, const AesLds& T, const RK& rk) {
+    template <class TT, class RK>
+    MH_D void refill_pair(ConvStream& o, const TT& T, const RK& rk) {
         if (half == 2 && o.half == 2) {
             fixed_key_block2(T, rk, seed, ctr, o.seed, o.ctr, blk, o.blk);
             ctr++;
@@ -211,8 +211,8 @@ template <> struct ConvStream<F64> {
             o.half = 0;
         }
     }
-    template <class RK>
-    MH_D uint64_t next(const AesLds& T, const RK& rk) {
+    template <class TT, class RK>
+    MH_D uint64_t next(const TT& T, const RK& rk) {
         uint64_t v;
         do {
             if (half == 2) {
@@ -237,8 +237,8 @@ template <> struct ConvStream<F128> {
         ctr = 1;
         have = 0;
     }
-    template <class RK>
-    MH_D void refill_pair(ConvStream& o, const AesLds& T, const RK& rk) {
+    template <class TT, class RK>
+    MH_D void refill_pair(ConvStream& o, const TT& T, const RK& rk) {
         if (!have && !o.have) {
             fixed_key_block2(T, rk, seed, ctr, o.seed, o.ctr, blk, o.blk);
             ctr++;
@@ -247,8 +247,8 @@ template <> struct ConvStream<F128> {
             o.have = 1;
         }
     }
-    template <class RK>
-    MH_D F128::E next(const AesLds& T, const RK& rk) {
+    template <class TT, class RK>
+    MH_D F128::E next(const TT& T, const RK& rk) {
         F128::E v;
         do {
             if (!have) {
@@ -289,17 +289,19 @@ struct AesArgs {
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
 };
 
-// One workgroup = 64 reports (one per lane) x 8 waves, each wave walking its
-// own run of parents.  LDS: the replicated T-table (32 KiB) and the 64
-// reports' two AES key schedules (22 KiB, one ds_read_b128 per round) are
-// shared by all 8 waves: 54 KiB per workgroup, 2 workgroups per CU.
+// One workgroup = 64 reports (one per lane) x 16 waves, each wave walking its
+// own run of parents.  LDS: the v_perm-addressed T0/T2 table (64 KiB,
+// aes.hpp AesPerm) and the 64 reports' two AES key schedules (22 KiB, one
+// ds_read_b128 per round) are shared by all 16 waves: 86 KiB per workgroup,
+// one workgroup = 4 waves per SIMD per CU.
+#define EVAL_WAVES 16
 template <class F>
-__global__ __launch_bounds__(512) void k_eval_aes(McParams p, Planes pl, AesArgs a) {
+__global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
-    __shared__ uint32_t T[AES_LDS_WORDS];
+    __shared__ uint32_t T[AES_PERM_LDS_WORDS];
     __shared__ uint4 RKE[64 * 11];
     __shared__ uint4 RKC[64 * 11];
-    aes_lds_fill(T, threadIdx.x, 512);
+    aes_perm_fill(T, threadIdx.x, 64 * EVAL_WAVES);
 
     const int S = pl.stride;
     const int lane = threadIdx.x & 63;
@@ -309,19 +311,19 @@ __global__ __launch_bounds__(512) void k_eval_aes(McParams p, Planes pl, AesArgs
     {
         uint32_t* ke = (uint32_t*)RKE;
         uint32_t* kc = (uint32_t*)RKC;
-        for (int i = wave; i < 44; i += 8) {
+        for (int i = wave; i < 44; i += EVAL_WAVES) {
             ke[lane * 44 + i] = pld(pl.rk_ext + (size_t)i * S, lb);
             kc[lane * 44 + i] = pld(pl.rk_conv + (size_t)i * S, lb);
         }
     }
     __syncthreads();
-    const int pbeg = (blockIdx.y * 8 + wave) * a.ppw;
+    const int pbeg = (blockIdx.y * EVAL_WAVES + wave) * a.ppw;
     if (pbeg >= a.n_parents) return;
     const int pend = min(pbeg + a.ppw, a.n_parents);
     const int l = a.level;
     const int vl = p.value_len;
     const int wl = vl * F::W32;
-    AesLds TL{T + (lane & 31)};
+    const AesPerm TL{T, 4u * (uint32_t)(lane & 31), 128u + 4u * (uint32_t)(lane & 31)};
     const RkLds rke{RKE + lane * 11};
     const RkLds rkc{RKC + lane * 11};
 

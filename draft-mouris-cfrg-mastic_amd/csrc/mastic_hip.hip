@@ -531,10 +531,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.fr_w_out = plane(wl.fr_w[l & 1]);
         a.payload = plane(wl.payload[slot]);
         a.out = plane(wl.out);
-        dim3 grid(groups, (np_ + 8 * a.ppw - 1) / (8 * a.ppw));
+        dim3 grid(groups, (np_ + EVAL_WAVES * a.ppw - 1) / (EVAL_WAVES * a.ppw));
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        hipLaunchKernelGGL(k_eval_aes<F>, grid, dim3(512), 0, c->stream, p, pl, a);
+        hipLaunchKernelGGL(k_eval_aes<F>, grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipGetLastError());
         hipEvent_t aes_done = get_sync_event(c, sev++);
