@@ -207,7 +207,7 @@ MH_D void fixed_key_block2(const TT& T, const RK& rk, const uint32_t sa[4], uint
 // shift-add.  Banks stay conflict-free: lane l always reads bank l mod 32.
 // With T2 stored, a column needs one rotation instead of three:
 //   T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = T0[a] ^ T2[c] ^ rot8(T0[b] ^ T2[d]).
-// A round costs 16 v_perm + 4 x (xor, rot, xor3, xor) = 32 VALU against
+// A round costs 16 v_perm + 4 x (xor3, rot, xor3) = 28 VALU against
 // 52 with one rotated table and two-instruction addressing.
 #define AES_PERM_LDS_WORDS (256 * 64)
 
@@ -234,10 +234,17 @@ struct AesPerm {
     }
 };
 
-// One full round column: T0[b0(w0)] ^ T1[b1(w1)] ^ T2[b2(w2)] ^ T3[b3(w3)] ^ k
-MH_D uint32_t aes_col(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t k) {
-    const uint32_t r = rot8(T.t0<1>(w1) ^ T.t2<3>(w3));
-    return xor3_u32(T.t0<0>(w0), T.t2<2>(w2), r) ^ k;
+// One full round column: T0[b0(w0)] ^ T1[b1(w1)] ^ T2[b2(w2)] ^ T3[b3(w3)] ^ k,
+// given kr = rotr8(k):  T0[.] ^ T2[.] ^ rot8(T0[.] ^ T2[.] ^ kr)  — three VALU
+// after the four lookups.  Key schedules used with AesPerm therefore hold
+// rounds 1..9 rotated right by 8 (aes_perm_key_word); rounds 0 and 10 plain.
+MH_D uint32_t aes_col(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t kr) {
+    const uint32_t r = rot8(xor3_u32(T.t0<1>(w1), T.t2<3>(w3), kr));
+    return xor3_u32(T.t0<0>(w0), T.t2<2>(w2), r);
+}
+// Word i (< 44) of a key schedule as stored for AesPerm.
+MH_HD uint32_t aes_perm_key_word(int i, uint32_t w) {
+    return (i >= 4 && i < 40) ? ((w >> 8) | (w << 24)) : w;
 }
 // Final-round column: S-box bytes (byte 1 of the T0 entries) packed with two
 // v_perm_b32 and merged with the round key by one xor3.

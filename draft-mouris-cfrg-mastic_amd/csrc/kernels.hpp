@@ -312,8 +312,8 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
         uint32_t* ke = (uint32_t*)RKE;
         uint32_t* kc = (uint32_t*)RKC;
         for (int i = wave; i < 44; i += EVAL_WAVES) {
-            ke[lane * 44 + i] = pld(pl.rk_ext + (size_t)i * S, lb);
-            kc[lane * 44 + i] = pld(pl.rk_conv + (size_t)i * S, lb);
+            ke[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_ext + (size_t)i * S, lb));
+            kc[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_conv + (size_t)i * S, lb));
         }
     }
     __syncthreads();
@@ -620,6 +620,8 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
 // itself (the plane offset h*S is part of its per-lane buffer offset).
 __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     __builtin_amdgcn_s_setprio(3);
+    // (launched with optional dynamic LDS that is never touched: it only caps
+    // how many absorb workgroups share a CU, see mastic_ctx::absorb_lds)
     const int h = threadIdx.x & 1;
     const int r = blockIdx.x * 128 + (threadIdx.x >> 1);
     const int which = blockIdx.y;

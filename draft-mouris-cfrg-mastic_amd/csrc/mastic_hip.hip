@@ -92,6 +92,7 @@ struct mastic_ctx {
     DevBuf consts;   // alpha^-i table for prove
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
+    int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
@@ -572,7 +573,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e4, c->stream2));
         if (c->absorb_pair)
-            hipLaunchKernelGGL(k_absorb_pair, dim3((stride + 127) / 128, 2), dim3(256), 0, c->stream2, pl, ab);
+            hipLaunchKernelGGL(k_absorb_pair, dim3((stride + 127) / 128, 2), dim3(256), c->absorb_lds, c->stream2, pl,
+                               ab);
         else
             hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
         HIPCHK(c, hipEventRecord(e5, c->stream2));
@@ -1097,9 +1099,15 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     {
         const char* e = getenv("MASTIC_ABSORB_SINGLE");
         c->absorb_pair = !(e && e[0] == '1');
+        const char* l = getenv("MASTIC_ABSORB_LDS_KB");
+        c->absorb_lds = l ? std::max(0, std::min(64, atoi(l))) * 1024 : 0;
     }
+    // the binder sponges are the latency-critical chain: their stream gets the
+    // highest priority so their workgroups are dispatched first
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MASTIC_EHIP;
