@@ -299,3 +299,65 @@ MH_D void aes128_encrypt(const AesPerm& T, const RK& rk, uint32_t s[4]) {
     s[2] = aes_col_last(T, s2, s3, s0, s1, k.z);
     s[3] = aes_col_last(T, s3, s0, s1, s2, k.w);
 }
+
+// N blocks in lockstep (N = 4 for the payload stream of two sibling nodes):
+// a round issues 16 N independent lookups per wave, which keeps the LDS pipe
+// fed from fewer waves (the level kernel is LDS-latency bound at 4 waves/SIMD).
+template <int N, class RK>
+MH_D void aes128_encrypt_n(const AesPerm& T, const RK& rk, uint32_t (&x)[N][4]) {
+    uint4 k = rk(0);
+    uint32_t s[N][4];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        s[j][0] = x[j][0] ^ k.x;
+        s[j][1] = x[j][1] ^ k.y;
+        s[j][2] = x[j][2] ^ k.z;
+        s[j][3] = x[j][3] ^ k.w;
+    }
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k = rk(r);
+        uint32_t t[N][4];
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            t[j][0] = aes_col(T, s[j][0], s[j][1], s[j][2], s[j][3], k.x);
+            t[j][1] = aes_col(T, s[j][1], s[j][2], s[j][3], s[j][0], k.y);
+            t[j][2] = aes_col(T, s[j][2], s[j][3], s[j][0], s[j][1], k.z);
+            t[j][3] = aes_col(T, s[j][3], s[j][0], s[j][1], s[j][2], k.w);
+        }
+#pragma unroll
+        for (int j = 0; j < N; j++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) s[j][c] = t[j][c];
+    }
+    k = rk(10);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        x[j][0] = aes_col_last(T, s[j][0], s[j][1], s[j][2], s[j][3], k.x);
+        x[j][1] = aes_col_last(T, s[j][1], s[j][2], s[j][3], s[j][0], k.y);
+        x[j][2] = aes_col_last(T, s[j][2], s[j][3], s[j][0], s[j][1], k.z);
+        x[j][3] = aes_col_last(T, s[j][3], s[j][0], s[j][1], s[j][2], k.w);
+    }
+}
+
+// XofFixedKeyAes128 blocks (seed[j], ctr[j]) for j < N, in lockstep.
+template <int N, class RK>
+MH_D void fixed_key_block_n(const AesPerm& T, const RK& rk, const uint32_t* const (&seed)[N],
+                            const uint32_t (&ctr)[N], uint32_t* const (&out)[N]) {
+    uint32_t g[N][4], x[N][4];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t* sd = seed[j];
+        g[j][0] = sd[2];
+        g[j][1] = sd[3];
+        g[j][2] = sd[2] ^ sd[0] ^ ctr[j];
+        g[j][3] = sd[3] ^ sd[1];
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[j][c] = g[j][c];
+    }
+    aes128_encrypt_n<N>(T, rk, x);
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) out[j][c] = x[j][c] ^ g[j][c];
+}

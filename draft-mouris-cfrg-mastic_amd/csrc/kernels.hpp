@@ -227,6 +227,68 @@ template <> struct ConvStream<F64> {
     }
 };
 
+// Field64 stream of the level kernel: up to four candidates (two blocks)
+// buffered per node, so two sibling streams refill with ONE 4-block lockstep
+// AES call (fixed_key_block_n<4>); the last refill of a node (at most two
+// elements still needed) is a paired call of one block per sibling.  A stream
+// that rejected a candidate (probability ~2^-32) falls out of step with its
+// sibling and refills alone, block by block, exactly as the reference's
+// next_vec does.
+struct ConvQuad {
+    uint32_t seed[4];
+    uint32_t blk[8];  // candidate i = blk[2i] | blk[2i+1] << 32
+    uint32_t ctr;
+    uint32_t pos;     // next candidate slot, 4 = empty
+    MH_D void init(const uint32_t s[4]) {
+        seed[0] = s[0]; seed[1] = s[1]; seed[2] = s[2]; seed[3] = s[3];
+        ctr = 1;
+        pos = 4;
+    }
+    template <class RK>
+    MH_D void refill(ConvQuad& o, int remaining, const AesPerm& T, const RK& rk) {
+        if (pos == 4 && o.pos == 4) {
+            if (remaining > 2) {
+                const uint32_t* const sd[4] = {seed, seed, o.seed, o.seed};
+                const uint32_t cv[4] = {ctr, ctr + 1, o.ctr, o.ctr + 1};
+                uint32_t* const ov[4] = {blk, blk + 4, o.blk, o.blk + 4};
+                fixed_key_block_n<4>(T, rk, sd, cv, ov);
+                ctr += 2;
+                o.ctr += 2;
+                pos = 0;
+                o.pos = 0;
+            } else {
+                const uint32_t* const sd[2] = {seed, o.seed};
+                const uint32_t cv[2] = {ctr, o.ctr};
+                uint32_t* const ov[2] = {blk + 4, o.blk + 4};
+                fixed_key_block_n<2>(T, rk, sd, cv, ov);
+                ctr++;
+                o.ctr++;
+                pos = 2;
+                o.pos = 2;
+            }
+        }
+    }
+    template <class RK>
+    MH_D uint64_t next(const AesPerm& T, const RK& rk) {
+        uint64_t v;
+        do {
+            if (pos == 4) {
+                const uint32_t* const sd[1] = {seed};
+                const uint32_t cv[1] = {ctr};
+                uint32_t* const ov[1] = {blk + 4};
+                fixed_key_block_n<1>(T, rk, sd, cv, ov);
+                ctr++;
+                pos = 2;
+            }
+            const uint32_t lo = pos == 0 ? blk[0] : pos == 1 ? blk[2] : pos == 2 ? blk[4] : blk[6];
+            const uint32_t hi = pos == 0 ? blk[1] : pos == 1 ? blk[3] : pos == 2 ? blk[5] : blk[7];
+            v = ((uint64_t)hi << 32) | lo;
+            pos++;
+        } while (!F64::valid(v));
+        return v;
+    }
+};
+
 template <> struct ConvStream<F128> {
     uint32_t seed[4];
     uint32_t blk[4];
@@ -236,6 +298,10 @@ template <> struct ConvStream<F128> {
         seed[0] = s[0]; seed[1] = s[1]; seed[2] = s[2]; seed[3] = s[3];
         ctr = 1;
         have = 0;
+    }
+    template <class TT, class RK>
+    MH_D void refill(ConvStream& o, int, const TT& T, const RK& rk) {
+        refill_pair(o, T, rk);
     }
     template <class TT, class RK>
     MH_D void refill_pair(ConvStream& o, const TT& T, const RK& rk) {
@@ -261,6 +327,9 @@ template <> struct ConvStream<F128> {
         return v;
     }
 };
+
+template <class F> struct EvalStream { typedef ConvStream<F> type; };
+template <> struct EvalStream<F64> { typedef ConvQuad type; };
 
 // ------------------------------------------------------------- eval level
 // A tree level is evaluated by two kernels:
@@ -380,14 +449,14 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
         // payloads of both children, element by element
-        ConvStream<F> st0, st1;
+        typename EvalStream<F>::type st0, st1;
         st0.init(cs0);
         st1.init(cs1);
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         const int row = 1 + p.output_len;
         for (int e = 0; e < vl; e++) {
             asm volatile("" ::: "memory");
-            st0.refill_pair(st1, TL, rkc);
+            st0.refill(st1, vl - e, TL, rkc);
             E x0 = st0.next(TL, rkc);
             E x1 = st1.next(TL, rkc);
             E cw = pl_load<F>(wcw, e, S, r);
