@@ -235,6 +235,7 @@ template <> struct ConvStream<F64> {
 // sibling and refills alone, block by block, exactly as the reference's
 // next_vec does.
 struct ConvQuad {
+    static constexpr int GROUP = 4;  // candidates per refill
     uint32_t seed[4];
     uint32_t blk[8];  // candidate i = blk[2i] | blk[2i+1] << 32
     uint32_t ctr;
@@ -289,6 +290,64 @@ struct ConvQuad {
     }
 };
 
+// Field128 counterpart: one candidate per block, two buffered per node.
+struct ConvQuad128 {
+    static constexpr int GROUP = 2;
+    uint32_t seed[4];
+    uint32_t blk[8];  // candidate i = blk[4i .. 4i+3]
+    uint32_t ctr;
+    uint32_t pos;     // next candidate slot, 2 = empty
+    MH_D void init(const uint32_t s[4]) {
+        seed[0] = s[0]; seed[1] = s[1]; seed[2] = s[2]; seed[3] = s[3];
+        ctr = 1;
+        pos = 2;
+    }
+    template <class RK>
+    MH_D void refill(ConvQuad128& o, int remaining, const AesPerm& T, const RK& rk) {
+        if (pos == 2 && o.pos == 2) {
+            if (remaining > 1) {
+                const uint32_t* const sd[4] = {seed, seed, o.seed, o.seed};
+                const uint32_t cv[4] = {ctr, ctr + 1, o.ctr, o.ctr + 1};
+                uint32_t* const ov[4] = {blk, blk + 4, o.blk, o.blk + 4};
+                fixed_key_block_n<4>(T, rk, sd, cv, ov);
+                ctr += 2;
+                o.ctr += 2;
+                pos = 0;
+                o.pos = 0;
+            } else {
+                const uint32_t* const sd[2] = {seed, o.seed};
+                const uint32_t cv[2] = {ctr, o.ctr};
+                uint32_t* const ov[2] = {blk + 4, o.blk + 4};
+                fixed_key_block_n<2>(T, rk, sd, cv, ov);
+                ctr++;
+                o.ctr++;
+                pos = 1;
+                o.pos = 1;
+            }
+        }
+    }
+    template <class RK>
+    MH_D F128::E next(const AesPerm& T, const RK& rk) {
+        F128::E v;
+        do {
+            if (pos == 2) {
+                const uint32_t* const sd[1] = {seed};
+                const uint32_t cv[1] = {ctr};
+                uint32_t* const ov[1] = {blk + 4};
+                fixed_key_block_n<1>(T, rk, sd, cv, ov);
+                ctr++;
+                pos = 1;
+            }
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) w[i] = pos == 0 ? blk[i] : blk[4 + i];
+            v = F128::from_words(w);
+            pos++;
+        } while (!F128::valid(v));
+        return v;
+    }
+};
+
 template <> struct ConvStream<F128> {
     uint32_t seed[4];
     uint32_t blk[4];
@@ -328,8 +387,9 @@ template <> struct ConvStream<F128> {
     }
 };
 
-template <class F> struct EvalStream { typedef ConvStream<F> type; };
+template <class F> struct EvalStream;
 template <> struct EvalStream<F64> { typedef ConvQuad type; };
+template <> struct EvalStream<F128> { typedef ConvQuad128 type; };
 
 // ------------------------------------------------------------- eval level
 // A tree level is evaluated by two kernels:
@@ -402,14 +462,10 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
     const uint32_t ccw = pld(pl.cw_ctrl + (size_t)l * S, lb);
     const uint32_t* wcw = pl.cw_w + (size_t)l * wl * S;
 
-    for (int pi = pbeg; pi < pend; pi++) {
-        // The key schedules are re-read from LDS (one ds_read_b128 per round):
-        // without the barrier the compiler hoists all 22 reads out of the loop
-        // and pins 88 VGPRs.
-        asm volatile("" ::: "memory");
-        // parent seed / control bit
-        uint32_t ps[4];
-        uint32_t pctrl;
+    // Parent seed / control bit, software-pipelined one parent ahead so the
+    // HBM latency of the child-seed planes hides under the previous parent's
+    // AES work.
+    auto load_parent = [&](int pi, uint32_t* ps, uint32_t& pctrl) {
         if (l == 0) {
 #pragma unroll
             for (int i = 0; i < 4; i++) ps[i] = pld(pl.key + (size_t)i * S, lb);
@@ -420,6 +476,17 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
             for (int i = 0; i < 4; i++) ps[i] = pld(a.cs_in + ((size_t)pn * 5 + i) * S, lb);
             pctrl = pld(a.cs_in + ((size_t)pn * 5 + 4) * S, lb);
         }
+    };
+    uint32_t nps[4], npctrl;
+    load_parent(pbeg, nps, npctrl);
+    for (int pi = pbeg; pi < pend; pi++) {
+        // The key schedules are re-read from LDS (one ds_read_b128 per round):
+        // without the barrier the compiler hoists all 22 reads out of the loop
+        // and pins 88 VGPRs.
+        asm volatile("" ::: "memory");
+        uint32_t ps[4] = {nps[0], nps[1], nps[2], nps[3]};
+        const uint32_t pctrl = npctrl;
+        if (pi + 1 < pend) load_parent(pi + 1, nps, npctrl);
         // extend: block 0 -> left child, block 1 -> right child (one paired
         // AES call), correct, then both children's convert seed blocks.
         uint32_t cs0[4], cs1[4], ns0[4], ns1[4];
@@ -454,12 +521,27 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
         st1.init(cs1);
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         const int row = 1 + p.output_len;
-        for (int e = 0; e < vl; e++) {
+        // Elements in groups of one refill: the group's payload-CW and
+        // parent-payload loads are issued before its AES so their latency
+        // hides under it.
+        constexpr int G = EvalStream<F>::type::GROUP;
+        for (int e0 = 0; e0 < vl; e0 += G) {
             asm volatile("" ::: "memory");
-            st0.refill(st1, vl - e, TL, rkc);
+            E cwv[G], wpv[G];
+#pragma unroll
+            for (int i = 0; i < G; i++) {
+                const int ec = min(e0 + i, vl - 1);  // uniform clamp; duplicate loads are unused
+                cwv[i] = pl_load<F>(wcw, ec, S, r);
+                wpv[i] = l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + ec, S, r) : F::zero();
+            }
+            st0.refill(st1, vl - e0, TL, rkc);
+#pragma unroll
+            for (int i = 0; i < G; i++) {
+            const int e = e0 + i;
+            if (e >= vl) break;
             E x0 = st0.next(TL, rkc);
             E x1 = st1.next(TL, rkc);
-            E cw = pl_load<F>(wcw, e, S, r);
+            const E cw = cwv[i];
             if (tc0) x0 = F::add(x0, cw);
             if (tc1) x1 = F::add(x1, cw);
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
@@ -467,8 +549,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
             if (l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
-                E wp = pl_load<F>(a.fr_w_in, pi * vl + e, S, r);
-                pl_store<F>(a.payload, pi * vl + e, S, r, F::sub(F::sub(wp, x0), x1));
+                pl_store<F>(a.payload, pi * vl + e, S, r, F::sub(F::sub(wpv[i], x0), x1));
             }
             if (pf0 >= 0 || pf1 >= 0) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
@@ -492,6 +573,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
                         if (pf1 >= 0) pl_store<F>(a.out, pf1 * row + o, S, r, a.agg_id ? F::neg(acc1) : acc1);
                     }
                 }
+            }
             }
         }
     }
