@@ -234,8 +234,9 @@ template <> struct ConvStream<F64> {
 // that rejected a candidate (probability ~2^-32) falls out of step with its
 // sibling and refills alone, block by block, exactly as the reference's
 // next_vec does.
+template <bool QUAD>
 struct ConvQuad {
-    static constexpr int GROUP = 4;  // candidates per refill
+    static constexpr int GROUP = QUAD ? 4 : 2;  // candidates per refill
     uint32_t seed[4];
     uint32_t blk[8];  // candidate i = blk[2i] | blk[2i+1] << 32
     uint32_t ctr;
@@ -248,7 +249,7 @@ struct ConvQuad {
     template <class RK>
     MH_D void refill(ConvQuad& o, int remaining, const AesPerm& T, const RK& rk) {
         if (pos == 4 && o.pos == 4) {
-            if (remaining > 2) {
+            if (QUAD && remaining > 2) {
                 const uint32_t* const sd[4] = {seed, seed, o.seed, o.seed};
                 const uint32_t cv[4] = {ctr, ctr + 1, o.ctr, o.ctr + 1};
                 uint32_t* const ov[4] = {blk, blk + 4, o.blk, o.blk + 4};
@@ -291,8 +292,9 @@ struct ConvQuad {
 };
 
 // Field128 counterpart: one candidate per block, two buffered per node.
+template <bool QUAD>
 struct ConvQuad128 {
-    static constexpr int GROUP = 2;
+    static constexpr int GROUP = QUAD ? 2 : 1;
     uint32_t seed[4];
     uint32_t blk[8];  // candidate i = blk[4i .. 4i+3]
     uint32_t ctr;
@@ -305,7 +307,7 @@ struct ConvQuad128 {
     template <class RK>
     MH_D void refill(ConvQuad128& o, int remaining, const AesPerm& T, const RK& rk) {
         if (pos == 2 && o.pos == 2) {
-            if (remaining > 1) {
+            if (QUAD && remaining > 1) {
                 const uint32_t* const sd[4] = {seed, seed, o.seed, o.seed};
                 const uint32_t cv[4] = {ctr, ctr + 1, o.ctr, o.ctr + 1};
                 uint32_t* const ov[4] = {blk, blk + 4, o.blk, o.blk + 4};
@@ -387,9 +389,9 @@ template <> struct ConvStream<F128> {
     }
 };
 
-template <class F> struct EvalStream;
-template <> struct EvalStream<F64> { typedef ConvQuad type; };
-template <> struct EvalStream<F128> { typedef ConvQuad128 type; };
+template <class F, bool QUAD> struct EvalStream;
+template <bool Q> struct EvalStream<F64, Q> { typedef ConvQuad<Q> type; };
+template <bool Q> struct EvalStream<F128, Q> { typedef ConvQuad128<Q> type; };
 
 // ------------------------------------------------------------- eval level
 // A tree level is evaluated by two kernels:
@@ -424,7 +426,9 @@ struct AesArgs {
 // ds_read_b128 per round) are shared by all 16 waves: 86 KiB per workgroup,
 // one workgroup = 4 waves per SIMD per CU.
 #define EVAL_WAVES 16
-template <class F>
+// QUAD: payload refills of 2 blocks per sibling (4-block lockstep AES) instead
+// of 1 (paired); chosen at run time (mastic_ctx::eval_quad).
+template <class F, bool QUAD>
 __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
     __shared__ uint32_t T[AES_PERM_LDS_WORDS];
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
         // payloads of both children, element by element
-        typename EvalStream<F>::type st0, st1;
+        typename EvalStream<F, QUAD>::type st0, st1;
         st0.init(cs0);
         st1.init(cs1);
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
@@ -524,7 +528,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
         // Elements in groups of one refill: the group's payload-CW and
         // parent-payload loads are issued before its AES so their latency
         // hides under it.
-        constexpr int G = EvalStream<F>::type::GROUP;
+        constexpr int G = EvalStream<F, QUAD>::type::GROUP;
         for (int e0 = 0; e0 < vl; e0 += G) {
             asm volatile("" ::: "memory");
             E cwv[G], wpv[G];

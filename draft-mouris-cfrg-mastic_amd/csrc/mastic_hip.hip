@@ -93,6 +93,7 @@ struct mastic_ctx {
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
+    bool eval_quad = false;     // 4-block payload refills in k_eval_aes (MASTIC_EVAL_QUAD=1)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
@@ -535,7 +536,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         dim3 grid(groups, (np_ + EVAL_WAVES * a.ppw - 1) / (EVAL_WAVES * a.ppw));
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        hipLaunchKernelGGL(k_eval_aes<F>, grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
+        if (c->eval_quad)
+            hipLaunchKernelGGL((k_eval_aes<F, true>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
+        else
+            hipLaunchKernelGGL((k_eval_aes<F, false>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipGetLastError());
         hipEvent_t aes_done = get_sync_event(c, sev++);
@@ -1101,6 +1105,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         c->absorb_pair = !(e && e[0] == '1');
         const char* l = getenv("MASTIC_ABSORB_LDS_KB");
         c->absorb_lds = l ? std::max(0, std::min(64, atoi(l))) * 1024 : 0;
+        const char* q = getenv("MASTIC_EVAL_QUAD");
+        c->eval_quad = q && q[0] == '1';
     }
     // the binder sponges are the latency-critical chain: their stream gets the
     // highest priority so their workgroups are dispatched first

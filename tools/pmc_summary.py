@@ -1,0 +1,60 @@
+"""Summarise a tools/profile_r01.sh output directory: per-kernel serialized
+duration (PMC passes), VALU / LDS utilisation, wave-state split, HBM bytes."""
+import collections
+import csv
+import json
+import os
+import sys
+
+CLK = 2.4e9
+CUS = 256
+
+
+def load(path):
+    rows = list(csv.DictReader(open(path)))
+    dur = collections.defaultdict(float)
+    n = collections.Counter()
+    seen = set()
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in rows:
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        k = k.split("<")[0] + ("<F128>" if "F128" in k else "<F64>" if "F64" in k else "")
+        if r["Dispatch_Id"] not in seen:
+            seen.add(r["Dispatch_Id"])
+            dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            n[k] += 1
+        vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    return dur, n, vals
+
+
+def main(d, kernels=("k_eval_aes<F64>", "k_node_proof", "k_absorb_pair", "k_absorb")):
+    out = {}
+    dur, n, sq1 = load(os.path.join(d, "sq1/run_counter_collection.csv"))
+    _, _, sq2 = load(os.path.join(d, "sq2/run_counter_collection.csv"))
+    _, _, fe = load(os.path.join(d, "fetch/run_counter_collection.csv"))
+    _, _, wr = load(os.path.join(d, "write/run_counter_collection.csv"))
+    for k in kernels:
+        if k not in dur:
+            continue
+        ms = dur[k]
+        cyc = ms / 1e3 * CLK
+        v1, v2 = sq1[k], sq2[k]
+        act = v2["SQ_ACTIVE_INST_ANY"] or 1.0
+        out[k] = {
+            "launches": n[k],
+            "serial_ms": ms,
+            "valu_busy": v1["SQ_INSTS_VALU"] * 4 / (cyc * CUS * 4),
+            "lds_busy": v2["SQ_LDS_IDX_ACTIVE"] / (cyc * CUS),
+            "wait_any_over_active": v2["SQ_WAIT_ANY"] / act,
+            "wait_inst_any_over_active": v2["SQ_WAIT_INST_ANY"] / act,
+            "wait_inst_lds_over_active": v2["SQ_WAIT_INST_LDS"] / act,
+            "valu_wave_instr": v1["SQ_INSTS_VALU"],
+            "lds_wave_instr": v1["SQ_INSTS_LDS"],
+            "hbm_read_bytes": 2 * fe[k]["FETCH_SIZE"] * 1024,  # KB units; gfx950 counts half (MI355X_MICROARCH.md)
+            "hbm_write_bytes": wr[k]["WRITE_SIZE"] * 1024,
+        }
+    return out
+
+
+if __name__ == "__main__":
+    print(json.dumps(main(sys.argv[1]), indent=1))
