@@ -254,90 +254,114 @@ MH_D uint32_t aes_col_last(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t 
     return xor3_u32(lo, hi, k);
 }
 
+// Middle rounds.  All 16 N table lookups of a round are issued before any is
+// consumed: an empty asm statement takes every lookup result as an operand,
+// so the compiler cannot interleave "two reads, wait, xor" (which it does
+// inside the level kernel when left alone, leaving 2 of the LDS pipe's reads
+// in flight per wave instead of 16 N).  One wait per round, then the XORs.
+#define MH_PIN16(L, o)                                                                                        \
+    "+v"(L[o + 0]), "+v"(L[o + 1]), "+v"(L[o + 2]), "+v"(L[o + 3]), "+v"(L[o + 4]), "+v"(L[o + 5]),           \
+        "+v"(L[o + 6]), "+v"(L[o + 7]), "+v"(L[o + 8]), "+v"(L[o + 9]), "+v"(L[o + 10]), "+v"(L[o + 11]),     \
+        "+v"(L[o + 12]), "+v"(L[o + 13]), "+v"(L[o + 14]), "+v"(L[o + 15])
+template <int N>
+MH_D void aes_pin(uint32_t (&L)[16 * N]) {
+    if constexpr (N == 1) {
+        asm volatile("" : MH_PIN16(L, 0));
+    } else if constexpr (N == 2) {
+        asm volatile("" : MH_PIN16(L, 0), MH_PIN16(L, 16));
+    } else {
+#pragma unroll
+        for (int j = 0; j + 1 < N; j += 2) asm volatile("" : MH_PIN16(L, 16 * j), MH_PIN16(L, 16 * j + 16));
+    }
+}
+
+// One middle round of N blocks; k holds the round key as stored for AesPerm
+// (rotated right by 8, see aes_perm_key_word).
+template <int N>
+MH_D void aes_round_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
+    uint32_t L[16 * N];
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            L[16 * j + 4 * c + 0] = T.t0<0>(s[j][c]);
+            L[16 * j + 4 * c + 1] = T.t0<1>(s[j][(c + 1) & 3]);
+            L[16 * j + 4 * c + 2] = T.t2<2>(s[j][(c + 2) & 3]);
+            L[16 * j + 4 * c + 3] = T.t2<3>(s[j][(c + 3) & 3]);
+        }
+    aes_pin<N>(L);
+    const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t* q = L + 16 * j + 4 * c;
+            s[j][c] = xor3_u32(q[0], q[2], rot8(xor3_u32(q[1], q[3], kk[c])));
+        }
+}
+
+// Final round of N blocks: S-box bytes (byte 1 of the T0 entries) packed with
+// two v_perm_b32 and merged with the round key by one xor3.
+template <int N>
+MH_D void aes_last_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
+    uint32_t L[16 * N];
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            L[16 * j + 4 * c + 0] = T.t0<0>(s[j][c]);
+            L[16 * j + 4 * c + 1] = T.t0<1>(s[j][(c + 1) & 3]);
+            L[16 * j + 4 * c + 2] = T.t0<2>(s[j][(c + 2) & 3]);
+            L[16 * j + 4 * c + 3] = T.t0<3>(s[j][(c + 3) & 3]);
+        }
+    aes_pin<N>(L);
+    const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t* q = L + 16 * j + 4 * c;
+            const uint32_t lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0501u);
+            const uint32_t hi = __builtin_amdgcn_perm(q[3], q[2], 0x05010c0cu);
+            s[j][c] = xor3_u32(lo, hi, kk[c]);
+        }
+}
+
+// N blocks in lockstep (N = 2: the two children of a parent; N = 4: two
+// payload blocks per sibling): a round issues 16 N independent lookups per
+// wave, which keeps the LDS pipe fed at 4 waves/SIMD.
+template <int N, class RK>
+MH_D void aes128_encrypt_n(const AesPerm& T, const RK& rk, uint32_t (&x)[N][4]) {
+    uint4 k = rk(0);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        x[j][0] ^= k.x;
+        x[j][1] ^= k.y;
+        x[j][2] ^= k.z;
+        x[j][3] ^= k.w;
+    }
+#pragma unroll
+    for (int r = 1; r < 10; r++) aes_round_n<N>(T, x, rk(r));
+    aes_last_n<N>(T, x, rk(10));
+}
+
 template <class RK>
 MH_D void aes128_encrypt2(const AesPerm& T, const RK& rk, uint32_t a[4], uint32_t b[4]) {
-    uint4 k = rk(0);
-    uint32_t a0 = a[0] ^ k.x, a1 = a[1] ^ k.y, a2 = a[2] ^ k.z, a3 = a[3] ^ k.w;
-    uint32_t c0 = b[0] ^ k.x, c1 = b[1] ^ k.y, c2 = b[2] ^ k.z, c3 = b[3] ^ k.w;
+    uint32_t x[2][4] = {{a[0], a[1], a[2], a[3]}, {b[0], b[1], b[2], b[3]}};
+    aes128_encrypt_n<2>(T, rk, x);
 #pragma unroll
-    for (int r = 1; r < 10; r++) {
-        k = rk(r);
-        const uint32_t t0 = aes_col(T, a0, a1, a2, a3, k.x), u0 = aes_col(T, c0, c1, c2, c3, k.x);
-        const uint32_t t1 = aes_col(T, a1, a2, a3, a0, k.y), u1 = aes_col(T, c1, c2, c3, c0, k.y);
-        const uint32_t t2 = aes_col(T, a2, a3, a0, a1, k.z), u2 = aes_col(T, c2, c3, c0, c1, k.z);
-        const uint32_t t3 = aes_col(T, a3, a0, a1, a2, k.w), u3 = aes_col(T, c3, c0, c1, c2, k.w);
-        a0 = t0; a1 = t1; a2 = t2; a3 = t3;
-        c0 = u0; c1 = u1; c2 = u2; c3 = u3;
+    for (int c = 0; c < 4; c++) {
+        a[c] = x[0][c];
+        b[c] = x[1][c];
     }
-    k = rk(10);
-    a[0] = aes_col_last(T, a0, a1, a2, a3, k.x);
-    b[0] = aes_col_last(T, c0, c1, c2, c3, k.x);
-    a[1] = aes_col_last(T, a1, a2, a3, a0, k.y);
-    b[1] = aes_col_last(T, c1, c2, c3, c0, k.y);
-    a[2] = aes_col_last(T, a2, a3, a0, a1, k.z);
-    b[2] = aes_col_last(T, c2, c3, c0, c1, k.z);
-    a[3] = aes_col_last(T, a3, a0, a1, a2, k.w);
-    b[3] = aes_col_last(T, c3, c0, c1, c2, k.w);
 }
 
 template <class RK>
 MH_D void aes128_encrypt(const AesPerm& T, const RK& rk, uint32_t s[4]) {
-    uint4 k = rk(0);
-    uint32_t s0 = s[0] ^ k.x, s1 = s[1] ^ k.y, s2 = s[2] ^ k.z, s3 = s[3] ^ k.w;
+    uint32_t x[1][4] = {{s[0], s[1], s[2], s[3]}};
+    aes128_encrypt_n<1>(T, rk, x);
 #pragma unroll
-    for (int r = 1; r < 10; r++) {
-        k = rk(r);
-        const uint32_t t0 = aes_col(T, s0, s1, s2, s3, k.x);
-        const uint32_t t1 = aes_col(T, s1, s2, s3, s0, k.y);
-        const uint32_t t2 = aes_col(T, s2, s3, s0, s1, k.z);
-        const uint32_t t3 = aes_col(T, s3, s0, s1, s2, k.w);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-    k = rk(10);
-    s[0] = aes_col_last(T, s0, s1, s2, s3, k.x);
-    s[1] = aes_col_last(T, s1, s2, s3, s0, k.y);
-    s[2] = aes_col_last(T, s2, s3, s0, s1, k.z);
-    s[3] = aes_col_last(T, s3, s0, s1, s2, k.w);
-}
-
-// N blocks in lockstep (N = 4 for the payload stream of two sibling nodes):
-// a round issues 16 N independent lookups per wave, which keeps the LDS pipe
-// fed from fewer waves (the level kernel is LDS-latency bound at 4 waves/SIMD).
-template <int N, class RK>
-MH_D void aes128_encrypt_n(const AesPerm& T, const RK& rk, uint32_t (&x)[N][4]) {
-    uint4 k = rk(0);
-    uint32_t s[N][4];
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-        s[j][0] = x[j][0] ^ k.x;
-        s[j][1] = x[j][1] ^ k.y;
-        s[j][2] = x[j][2] ^ k.z;
-        s[j][3] = x[j][3] ^ k.w;
-    }
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        k = rk(r);
-        uint32_t t[N][4];
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            t[j][0] = aes_col(T, s[j][0], s[j][1], s[j][2], s[j][3], k.x);
-            t[j][1] = aes_col(T, s[j][1], s[j][2], s[j][3], s[j][0], k.y);
-            t[j][2] = aes_col(T, s[j][2], s[j][3], s[j][0], s[j][1], k.z);
-            t[j][3] = aes_col(T, s[j][3], s[j][0], s[j][1], s[j][2], k.w);
-        }
-#pragma unroll
-        for (int j = 0; j < N; j++)
-#pragma unroll
-            for (int c = 0; c < 4; c++) s[j][c] = t[j][c];
-    }
-    k = rk(10);
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-        x[j][0] = aes_col_last(T, s[j][0], s[j][1], s[j][2], s[j][3], k.x);
-        x[j][1] = aes_col_last(T, s[j][1], s[j][2], s[j][3], s[j][0], k.y);
-        x[j][2] = aes_col_last(T, s[j][2], s[j][3], s[j][0], s[j][1], k.z);
-        x[j][3] = aes_col_last(T, s[j][3], s[j][0], s[j][1], s[j][2], k.w);
-    }
+    for (int c = 0; c < 4; c++) s[c] = x[0][c];
 }
 
 // XofFixedKeyAes128 blocks (seed[j], ctr[j]) for j < N, in lockstep.

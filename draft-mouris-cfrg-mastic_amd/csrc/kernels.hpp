@@ -418,6 +418,7 @@ struct AesArgs {
     uint32_t* fr_w_out;
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
+    int force_slow_blk;  // test hook: the Field64 fast path hands over to the exact stream at this block (-1 = never)
 };
 
 // One workgroup = 64 reports (one per lane) x 16 waves, each wave walking its
@@ -428,8 +429,11 @@ struct AesArgs {
 #define EVAL_WAVES 16
 // QUAD: payload refills of 2 blocks per sibling (4-block lockstep AES) instead
 // of 1 (paired); chosen at run time (mastic_ctx::eval_quad).
-template <class F, bool QUAD>
-__global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes pl, AesArgs a) {
+// DBG (timing experiments only, results wrong): 1 = no payload-CW / parent
+// payload loads, 2 = no payload-phase stores, 4 = no payload phase at all.
+template <class F, bool QUAD, int DBG = 0>
+__global__ __launch_bounds__(64 * EVAL_WAVES) __attribute__((amdgpu_waves_per_eu(EVAL_WAVES / 4, EVAL_WAVES / 4)))
+void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
     __shared__ uint32_t T[AES_PERM_LDS_WORDS];
     __shared__ uint4 RKE[64 * 11];
@@ -519,41 +523,25 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
 
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
-        // payloads of both children, element by element
-        typename EvalStream<F, QUAD>::type st0, st1;
-        st0.init(cs0);
-        st1.init(cs1);
-        E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
+        if (DBG & 4) continue;
         const int row = 1 + p.output_len;
-        // Elements in groups of one refill: the group's payload-CW and
-        // parent-payload loads are issued before its AES so their latency
-        // hides under it.
-        constexpr int G = EvalStream<F, QUAD>::type::GROUP;
-        for (int e0 = 0; e0 < vl; e0 += G) {
-            asm volatile("" ::: "memory");
-            E cwv[G], wpv[G];
-#pragma unroll
-            for (int i = 0; i < G; i++) {
-                const int ec = min(e0 + i, vl - 1);  // uniform clamp; duplicate loads are unused
-                cwv[i] = pl_load<F>(wcw, ec, S, r);
-                wpv[i] = l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + ec, S, r) : F::zero();
-            }
-            st0.refill(st1, vl - e0, TL, rkc);
-#pragma unroll
-            for (int i = 0; i < G; i++) {
-            const int e = e0 + i;
-            if (e >= vl) break;
-            E x0 = st0.next(TL, rkc);
-            E x1 = st1.next(TL, rkc);
-            const E cw = cwv[i];
+        E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
+        // Element e of both children: payload correction, frontier payloads,
+        // the parent's payload difference (or the root sum), out shares.
+        auto emit = [&](int e, E x0, E x1, E cw, E wp) {
             if (tc0) x0 = F::add(x0, cw);
             if (tc1) x1 = F::add(x1, cw);
+            if (DBG & 2) {
+                acc0 = F::add(acc0, F::sub(F::sub(wp, x0), x1));
+                if (e == vl - 1 && F::is_zero(acc0)) pl_store<F>(a.payload, pi, S, r, acc0);
+                return;
+            }
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
             if (l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
-                pl_store<F>(a.payload, pi * vl + e, S, r, F::sub(F::sub(wpv[i], x0), x1));
+                pl_store<F>(a.payload, pi * vl + e, S, r, F::sub(F::sub(wp, x0), x1));
             }
             if (pf0 >= 0 || pf1 >= 0) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
@@ -578,6 +566,56 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void k_eval_aes(McParams p, Planes
                     }
                 }
             }
+        };
+        auto load_cw = [&](int e) { return (DBG & 1) ? F::from_u64(e) : pl_load<F>(wcw, e, S, r); };
+        auto load_wp = [&](int e) {
+            return (DBG & 1) ? F::from_u64(pi) : (l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + e, S, r) : F::zero());
+        };
+        int e_fast = 0;  // elements completed by the fast path
+        if constexpr (F::W32 == 2 && !QUAD) {
+            // Field64 fast path: block b (counter b + 1) of each child's convert
+            // stream holds candidates 2b and 2b + 1 (vdaf_poc next_vec after
+            // next(16)).  Speculate that no candidate is rejected: one paired AES
+            // call per block index, straight-line.  A candidate >= p has its high
+            // word 0xffffffff (probability 2^-32); if any lane of the wave sees
+            // such a word among the elements it is about to use, the exact
+            // stream below redoes this parent from that element on (elements
+            // before it are unaffected by the rejection).
+            const int nblk = (vl + 1) >> 1;
+            for (int b = 0; b < nblk; b++) {
+                asm volatile("" ::: "memory");
+                const int e = 2 * b;
+                const bool two = e + 1 < vl;
+                const int e1 = two ? e + 1 : e;  // uniform clamp
+                const E cwa = load_cw(e), cwb = load_cw(e1);
+                const E wpa = load_wp(e), wpb = load_wp(e1);
+                uint32_t o0[4], o1[4];
+                fixed_key_block2(TL, rkc, cs0, (uint32_t)(b + 1), cs1, (uint32_t)(b + 1), o0, o1);
+                const bool sus = (o0[1] == ~0u) | (o1[1] == ~0u) | (two & ((o0[3] == ~0u) | (o1[3] == ~0u)));
+                if (__builtin_expect(__any(sus), 0) || b == a.force_slow_blk) break;
+                emit(e, F::from_words(o0), F::from_words(o1), cwa, wpa);
+                if (two) emit(e + 1, F::from_words(o0 + 2), F::from_words(o1 + 2), cwb, wpb);
+                e_fast = e + 1 + (two ? 1 : 0);
+            }
+        }
+        if (e_fast < vl) {
+            // exact next_vec streams (rejection sampling), element by element
+            // from e_fast on; elements before it were emitted by the fast path
+            typename EvalStream<F, QUAD>::type st0, st1;
+            st0.init(cs0);
+            st1.init(cs1);
+            constexpr int G = EvalStream<F, QUAD>::type::GROUP;
+            for (int e0 = 0; e0 < vl; e0 += G) {
+                asm volatile("" ::: "memory");
+                st0.refill(st1, vl - e0, TL, rkc);
+#pragma unroll
+                for (int i = 0; i < G; i++) {
+                    const int e = e0 + i;
+                    if (e >= vl) break;
+                    const E x0 = st0.next(TL, rkc);
+                    const E x1 = st1.next(TL, rkc);
+                    if (e >= e_fast) emit(e, x0, x1, load_cw(e), load_wp(e));
+                }
             }
         }
     }

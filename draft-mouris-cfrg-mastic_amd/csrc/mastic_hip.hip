@@ -94,6 +94,8 @@ struct mastic_ctx {
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
     bool eval_quad = false;     // 4-block payload refills in k_eval_aes (MASTIC_EVAL_QUAD=1)
+    int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
+    int eval_dbg = 0;           // timing experiments only (MASTIC_EVAL_DBG, results wrong)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
@@ -533,10 +535,24 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.fr_w_out = plane(wl.fr_w[l & 1]);
         a.payload = plane(wl.payload[slot]);
         a.out = plane(wl.out);
+        a.force_slow_blk = c->force_slow_blk;
         dim3 grid(groups, (np_ + EVAL_WAVES * a.ppw - 1) / (EVAL_WAVES * a.ppw));
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        if (c->eval_quad)
+        bool launched = false;
+        if constexpr (F::W32 == 2) {
+            launched = true;
+            if (c->eval_dbg == 1)
+                hipLaunchKernelGGL((k_eval_aes<F, false, 1>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
+            else if (c->eval_dbg == 3)
+                hipLaunchKernelGGL((k_eval_aes<F, false, 3>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
+            else if (c->eval_dbg == 4)
+                hipLaunchKernelGGL((k_eval_aes<F, false, 4>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
+            else
+                launched = false;
+        }
+        if (launched) {
+        } else if (c->eval_quad)
             hipLaunchKernelGGL((k_eval_aes<F, true>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
         else
             hipLaunchKernelGGL((k_eval_aes<F, false>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
@@ -1107,6 +1123,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         c->absorb_lds = l ? std::max(0, std::min(64, atoi(l))) * 1024 : 0;
         const char* q = getenv("MASTIC_EVAL_QUAD");
         c->eval_quad = q && q[0] == '1';
+        const char* dbg = getenv("MASTIC_EVAL_DBG");
+        c->eval_dbg = dbg ? atoi(dbg) : 0;
+        const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
+        c->force_slow_blk = fs ? atoi(fs) : -1;
     }
     // the binder sponges are the latency-critical chain: their stream gets the
     // highest priority so their workgroups are dispatched first

@@ -15,6 +15,8 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(PKG_DIR, "libmastic_hip.so")
+# experiments only: load another build of the same library
+LOAD_PATH = os.environ.get("MASTIC_LIB", LIB_PATH)
 
 MASTIC_OK = 0
 ERRORS = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -5: "EHIP"}
@@ -85,10 +87,10 @@ def lib():
     if _lib is None:
         with _lock:
             if _lib is None:
-                if not os.path.exists(LIB_PATH):
+                if not os.path.exists(LOAD_PATH):
                     raise ImportError("libmastic_hip.so is not built (run __graft_entry__.build()); "
                                       "the HIP path has no CPU fallback")
-                l = ctypes.CDLL(LIB_PATH)
+                l = ctypes.CDLL(LOAD_PATH)
                 P = ctypes.c_void_p
                 u8p = ctypes.c_char_p
                 sz = ctypes.c_size_t

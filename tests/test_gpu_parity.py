@@ -345,3 +345,21 @@ def test_c2_shape_properties_and_oracle_sample(mastic_amd):
     (_st, sh) = o.prep_init(vk, CTX, 1, ap, nonces[:16], cws, isd)
     enc = o.test_vec_encode_prep_share(sh)
     assert res[1][0][:len(enc)] == enc
+
+
+@pytest.mark.parametrize("blk", [0, 1, 4, 8])
+def test_fast_path_handover_to_exact_stream(mastic_amd, blk, monkeypatch):
+    """The Field64 level kernel speculates that no next_vec candidate is
+    rejected and hands over to the exact rejection-sampling stream when one
+    might be (probability 2^-32 per candidate, never hit by random tests).
+    Force the handover at block `blk` and check every output against the
+    oracle: elements before the handover come from the fast path, the rest
+    from the exact stream."""
+    monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
+    rng = random.Random(100 + blk)
+    m = mastic_amd.MasticSum(6, 255)  # VALUE_LEN 17: 9 payload blocks per node
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 4)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    ap = _random_agg_param(m, rng, alphas, 5, 5, True)
+    _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=False)
