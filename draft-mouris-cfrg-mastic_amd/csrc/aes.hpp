@@ -219,20 +219,29 @@ MH_D void aes_perm_fill(uint32_t* T, int tid, int nthreads) {
 }
 
 struct AesPerm {
-    const uint32_t* T;  // the 64 KiB table
+    const uint32_t* T;  // the 64 KiB table; must sit at LDS address 0 (see lookup_n)
     uint32_t lb0;       // 4 * (lane & 31)
     uint32_t lb2;       // 128 + 4 * (lane & 31)
     template <int K>
-    MH_D uint32_t t0(uint32_t x) const {
-        const uint32_t a = __builtin_amdgcn_perm(x, lb0, 0x0c0c0000u | ((4u + K) << 8));
-        return *(const uint32_t*)((const char*)T + a);
-    }
+    MH_D uint32_t a0(uint32_t x) const { return __builtin_amdgcn_perm(x, lb0, 0x0c0c0000u | ((4u + K) << 8)); }
     template <int K>
-    MH_D uint32_t t2(uint32_t x) const {
-        const uint32_t a = __builtin_amdgcn_perm(x, lb2, 0x0c0c0000u | ((4u + K) << 8));
-        return *(const uint32_t*)((const char*)T + a);
-    }
+    MH_D uint32_t a2(uint32_t x) const { return __builtin_amdgcn_perm(x, lb2, 0x0c0c0000u | ((4u + K) << 8)); }
+    template <int K>
+    MH_D uint32_t t0(uint32_t x) const { return *(const uint32_t*)((const char*)T + a0<K>(x)); }
+    template <int K>
+    MH_D uint32_t t2(uint32_t x) const { return *(const uint32_t*)((const char*)T + a2<K>(x)); }
 };
+
+// LDS read of a table word at byte address a, issued as inline asm: the
+// v_perm result IS the LDS address (the table is the kernel's only LDS
+// block, at address 0), so no base add per lookup.  The compiler does not
+// track these reads; aes_pin<> waits for them (s_waitcnt lgkmcnt(0)) before
+// any result is used.
+MH_D uint32_t lds_read_asm(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
 
 // One full round column: T0[b0(w0)] ^ T1[b1(w1)] ^ T2[b2(w2)] ^ T3[b3(w3)] ^ k,
 // given kr = rotr8(k):  T0[.] ^ T2[.] ^ rot8(T0[.] ^ T2[.] ^ kr)  — three VALU
@@ -266,12 +275,14 @@ MH_D uint32_t aes_col_last(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t 
 template <int N>
 MH_D void aes_pin(uint32_t (&L)[16 * N]) {
     if constexpr (N == 1) {
-        asm volatile("" : MH_PIN16(L, 0));
+        asm volatile("s_waitcnt lgkmcnt(0)" : MH_PIN16(L, 0));
     } else if constexpr (N == 2) {
-        asm volatile("" : MH_PIN16(L, 0), MH_PIN16(L, 16));
+        asm volatile("s_waitcnt lgkmcnt(0)" : MH_PIN16(L, 0), MH_PIN16(L, 16));
     } else {
+        static_assert(N % 2 == 0, "N = 1, 2 or even");
 #pragma unroll
-        for (int j = 0; j + 1 < N; j += 2) asm volatile("" : MH_PIN16(L, 16 * j), MH_PIN16(L, 16 * j + 16));
+        for (int j = 0; j + 1 < N; j += 2)
+            asm volatile("s_waitcnt lgkmcnt(0)" : MH_PIN16(L, 16 * j), MH_PIN16(L, 16 * j + 16));
     }
 }
 
@@ -284,10 +295,10 @@ MH_D void aes_round_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
     for (int j = 0; j < N; j++)
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            L[16 * j + 4 * c + 0] = T.t0<0>(s[j][c]);
-            L[16 * j + 4 * c + 1] = T.t0<1>(s[j][(c + 1) & 3]);
-            L[16 * j + 4 * c + 2] = T.t2<2>(s[j][(c + 2) & 3]);
-            L[16 * j + 4 * c + 3] = T.t2<3>(s[j][(c + 3) & 3]);
+            L[16 * j + 4 * c + 0] = lds_read_asm(T.a0<0>(s[j][c]));
+            L[16 * j + 4 * c + 1] = lds_read_asm(T.a0<1>(s[j][(c + 1) & 3]));
+            L[16 * j + 4 * c + 2] = lds_read_asm(T.a2<2>(s[j][(c + 2) & 3]));
+            L[16 * j + 4 * c + 3] = lds_read_asm(T.a2<3>(s[j][(c + 3) & 3]));
         }
     aes_pin<N>(L);
     const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
@@ -309,10 +320,10 @@ MH_D void aes_last_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
     for (int j = 0; j < N; j++)
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            L[16 * j + 4 * c + 0] = T.t0<0>(s[j][c]);
-            L[16 * j + 4 * c + 1] = T.t0<1>(s[j][(c + 1) & 3]);
-            L[16 * j + 4 * c + 2] = T.t0<2>(s[j][(c + 2) & 3]);
-            L[16 * j + 4 * c + 3] = T.t0<3>(s[j][(c + 3) & 3]);
+            L[16 * j + 4 * c + 0] = lds_read_asm(T.a0<0>(s[j][c]));
+            L[16 * j + 4 * c + 1] = lds_read_asm(T.a0<1>(s[j][(c + 1) & 3]));
+            L[16 * j + 4 * c + 2] = lds_read_asm(T.a0<2>(s[j][(c + 2) & 3]));
+            L[16 * j + 4 * c + 3] = lds_read_asm(T.a0<3>(s[j][(c + 3) & 3]));
         }
     aes_pin<N>(L);
     const uint32_t kk[4] = {k.x, k.y, k.z, k.w};

@@ -393,6 +393,74 @@ template <class F, bool QUAD> struct EvalStream;
 template <bool Q> struct EvalStream<F64, Q> { typedef ConvQuad<Q> type; };
 template <bool Q> struct EvalStream<F128, Q> { typedef ConvQuad128<Q> type; };
 
+// ------------------------------------------------------------- node proof body
+#define NP_WIN 14
+template <int Q>
+MH_D void np_xor_window(KState& s, const uint32_t* x) {
+#pragma unroll
+    for (int k = 0; k < NP_WIN; k++)
+        if (Q + k < KECCAK_RATE_WORDS) kxor_word(s, Q + k, x[k]);
+}
+template <int Q>
+MH_D void np_xor_overflow(KState& s, const uint32_t* x) {
+#pragma unroll
+    for (int k = 0; k < NP_WIN; k++)
+        if (Q + k >= KECCAK_RATE_WORDS) kxor_word(s, Q + k - KECCAK_RATE_WORDS, x[k]);
+}
+#define NP_CASES(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) \
+    M(15) M(16) M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) \
+    M(31) M(32) M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40) M(41)
+
+// One node proof: TurboSHAKE128 over the pre-absorbed prefix state np (fill
+// position f) and the body  seed || le16(BITS) || le16(level) || path,
+// XORed with the level's proof correction word when the node's control bit
+// t is set.  Writes 8 words through `put(j, w)`.  All positions uniform.
+template <class Put>
+MH_D void node_proof_one(const PrefixState* np, int f, int bits, int level, int path_bytes, const uint32_t seed[4],
+                         const uint32_t* path, uint32_t t, const uint32_t pcw[8], Put put) {
+    const int q = f >> 2;
+    const int sh = f & 3;
+    const int nbytes = 20 + path_bytes;  // body; the domain byte 0x01 follows
+    const bool cross = f + nbytes >= KECCAK_RATE;
+    const uint32_t amt = (32 - 8 * sh) & 31;
+    const int dw = nbytes >> 2;
+    const uint32_t dbit = 1u << (8 * (nbytes & 3));
+    uint32_t B[NP_WIN];
+#pragma unroll
+    for (int i = 0; i < 4; i++) B[i] = seed[i];
+    B[4] = (uint32_t)bits | ((uint32_t)level << 16);
+#pragma unroll
+    for (int k = 5; k < NP_WIN; k++) B[k] = k - 5 < 8 ? path[k - 5] : 0u;
+#pragma unroll
+    for (int k = 4; k < NP_WIN; k++) B[k] |= (k == dw) ? dbit : 0u;
+    uint32_t x[NP_WIN];
+#pragma unroll
+    for (int k = 0; k < NP_WIN; k++) {
+        const uint32_t hi = B[k];
+        const uint32_t lo = k ? B[k - 1] : 0u;
+        x[k] = sh ? __builtin_amdgcn_alignbit(hi, lo, amt) : hi;
+    }
+    asm volatile("" ::: "memory");  // re-read the uniform prefix state, do not pin 50 registers
+    KState s = np->st;
+    switch (q) {
+#define NP_W(Q) case Q: np_xor_window<Q>(s, x); break;
+        NP_CASES(NP_W)
+#undef NP_W
+    }
+    if (cross) {
+        keccak_p12(s);
+        switch (q) {
+#define NP_O(Q) case Q: np_xor_overflow<Q>(s, x); break;
+            NP_CASES(NP_O)
+#undef NP_O
+        }
+    }
+    s.a[20].hi ^= 0x80000000u;
+    keccak_p12(s);
+#pragma unroll
+    for (int j = 0; j < 8; j++) put(j, kword(s, j) ^ (t ? pcw[j] : 0u));
+}
+
 // ------------------------------------------------------------- eval level
 // A tree level is evaluated by two kernels:
 //   k_eval_aes    extend + correct + convert of both children of every parent
@@ -419,25 +487,55 @@ struct AesArgs {
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
     int force_slow_blk;  // test hook: the Field64 fast path hands over to the exact stream at this block (-1 = never)
+    // node proofs of the PREVIOUS level (vidpf.py:366-380, :321-323), computed
+    // by the workgroup's EVAL_PROOF_WAVES proof waves beside the AES waves
+    int pv_level;                   // level - 1
+    int pv_nodes;                   // its node count (0 at level 0)
+    int pv_npw;                     // nodes per proof wave
+    int pv_path_bytes;              // ceil(level / 8)
+    const uint32_t* pv_child_path;  // [pv_nodes][8]
+    uint32_t* pv_onehot;            // [pv_nodes * 8] proof planes of level - 1
+    const PrefixState* np;          // node-proof prefix state
+    int np_f;                       // its fill position
+    int aes_waves;                  // waves [0, aes_waves) walk parents, the rest are proof waves
+    int proof_prio;                 // s_setprio of the proof waves
 };
 
-// One workgroup = 64 reports (one per lane) x 16 waves, each wave walking its
-// own run of parents.  LDS: the v_perm-addressed T0/T2 table (64 KiB,
+// One workgroup = 64 reports (one per lane) x 16 waves: 12 AES waves, each
+// walking its own run of this level's parents, and 4 proof waves computing
+// the node proofs of the previous level's children (a Keccak-p per node,
+// VALU only).  Specialised waves put LDS-bound AES and VALU-bound Keccak on
+// every CU at a fixed ratio, in one launch, instead of two kernels competing
+// for CU slots.  LDS: the v_perm-addressed T0/T2 table (64 KiB,
 // aes.hpp AesPerm) and the 64 reports' two AES key schedules (22 KiB, one
 // ds_read_b128 per round) are shared by all 16 waves: 86 KiB per workgroup,
 // one workgroup = 4 waves per SIMD per CU.
 #define EVAL_WAVES 16
+#define EVAL_PROOF_WAVES 4  // default split (mastic_ctx::proof_waves)
+// VGPR cap of the level kernel: 4 waves x 96 per SIMD leave 128 of the 512
+// for one binder-sponge wave (k_absorb_pair), so the two kernels can share a
+// CU instead of taking turns.
+// (expressed as a minimum occupancy: 5 waves/SIMD <=> at most 96 VGPRs)
+#ifndef EVAL_MIN_WAVES
+#define EVAL_MIN_WAVES 5
+#endif
+#define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(EVAL_MIN_WAVES)))
+#define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16)
 // QUAD: payload refills of 2 blocks per sibling (4-block lockstep AES) instead
 // of 1 (paired); chosen at run time (mastic_ctx::eval_quad).
-// DBG (timing experiments only, results wrong): 1 = no payload-CW / parent
-// payload loads, 2 = no payload-phase stores, 4 = no payload phase at all.
-template <class F, bool QUAD, int DBG = 0>
-__global__ __launch_bounds__(64 * EVAL_WAVES) __attribute__((amdgpu_waves_per_eu(EVAL_WAVES / 4, EVAL_WAVES / 4)))
+template <class F, bool QUAD>
+__global__ __launch_bounds__(64 * EVAL_WAVES) EVAL_VGPR_ATTR
 void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
-    __shared__ uint32_t T[AES_PERM_LDS_WORDS];
-    __shared__ uint4 RKE[64 * 11];
-    __shared__ uint4 RKC[64 * 11];
+    // dynamic LDS (EVAL_LDS_BYTES): with a static size the compiler derives
+    // the occupancy from it and ignores the VGPR cap of EVAL_VGPR_ATTR
+    extern __shared__ uint4 eval_lds[];
+    uint32_t* T = (uint32_t*)eval_lds;
+    uint4* RKE = eval_lds + AES_PERM_LDS_WORDS / 4;
+    uint4* RKC = RKE + 64 * 11;
+    // the T-table lookups use the v_perm result as the absolute LDS address
+    // (aes.hpp lds_read_asm): the table must start at LDS address 0
+    if ((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)eval_lds != 0u) __builtin_trap();
     aes_perm_fill(T, threadIdx.x, 64 * EVAL_WAVES);
 
     const int S = pl.stride;
@@ -454,7 +552,30 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         }
     }
     __syncthreads();
-    const int pbeg = (blockIdx.y * EVAL_WAVES + wave) * a.ppw;
+    const int aes_waves = a.aes_waves;
+    if (wave >= aes_waves) {
+        // proof wave: node proofs of level - 1 (children seeds from cs_in)
+        if (a.pv_nodes == 0) return;
+        if (a.proof_prio == 1) __builtin_amdgcn_s_setprio(1);
+        if (a.proof_prio == 2) __builtin_amdgcn_s_setprio(2);
+        const int nbeg = (blockIdx.y * (EVAL_WAVES - aes_waves) + (wave - aes_waves)) * a.pv_npw;
+        if (nbeg >= a.pv_nodes) return;
+        const int nend = min(nbeg + a.pv_npw, a.pv_nodes);
+        const int pl_ = a.pv_level;
+        uint32_t pcw[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)pl_ * 8 + j) * S, lb);
+        for (int node = nbeg; node < nend; node++) {
+            uint32_t sd[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_in + ((size_t)node * 5 + i) * S, lb);
+            const uint32_t t = pld(a.cs_in + ((size_t)node * 5 + 4) * S, lb);
+            node_proof_one(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
+                           [&](int j, uint32_t w) { pst(a.pv_onehot + ((size_t)node * 8 + j) * S, lb, w); });
+        }
+        return;
+    }
+    const int pbeg = (blockIdx.y * aes_waves + wave) * a.ppw;
     if (pbeg >= a.n_parents) return;
     const int pend = min(pbeg + a.ppw, a.n_parents);
     const int l = a.level;
@@ -520,10 +641,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         }
         pst(a.cs_out + (n0 + 4) * S, lb, tc0);
         pst(a.cs_out + (n1 + 4) * S, lb, tc1);
-
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
-        if (DBG & 4) continue;
         const int row = 1 + p.output_len;
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         // Element e of both children: payload correction, frontier payloads,
@@ -531,11 +650,6 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         auto emit = [&](int e, E x0, E x1, E cw, E wp) {
             if (tc0) x0 = F::add(x0, cw);
             if (tc1) x1 = F::add(x1, cw);
-            if (DBG & 2) {
-                acc0 = F::add(acc0, F::sub(F::sub(wp, x0), x1));
-                if (e == vl - 1 && F::is_zero(acc0)) pl_store<F>(a.payload, pi, S, r, acc0);
-                return;
-            }
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
             if (l == 0) {
@@ -567,10 +681,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 }
             }
         };
-        auto load_cw = [&](int e) { return (DBG & 1) ? F::from_u64(e) : pl_load<F>(wcw, e, S, r); };
-        auto load_wp = [&](int e) {
-            return (DBG & 1) ? F::from_u64(pi) : (l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + e, S, r) : F::zero());
-        };
+        auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
+        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + e, S, r) : F::zero(); };
         int e_fast = 0;  // elements completed by the fast path
         if constexpr (F::W32 == 2 && !QUAD) {
             // Field64 fast path: block b (counter b + 1) of each child's convert
@@ -640,23 +752,6 @@ struct ProofArgs {
     int f;                       // its fill position
 };
 
-#define NP_WIN 14
-template <int Q>
-MH_D void np_xor_window(KState& s, const uint32_t* x) {
-#pragma unroll
-    for (int k = 0; k < NP_WIN; k++)
-        if (Q + k < KECCAK_RATE_WORDS) kxor_word(s, Q + k, x[k]);
-}
-template <int Q>
-MH_D void np_xor_overflow(KState& s, const uint32_t* x) {
-#pragma unroll
-    for (int k = 0; k < NP_WIN; k++)
-        if (Q + k >= KECCAK_RATE_WORDS) kxor_word(s, Q + k - KECCAK_RATE_WORDS, x[k]);
-}
-#define NP_CASES(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) \
-    M(15) M(16) M(17) M(18) M(19) M(20) M(21) M(22) M(23) M(24) M(25) M(26) M(27) M(28) M(29) M(30) \
-    M(31) M(32) M(33) M(34) M(35) M(36) M(37) M(38) M(39) M(40) M(41)
-
 __global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, ProofArgs a) {
     const int S = pl.stride;
     const int lane = threadIdx.x & 63;
@@ -670,52 +765,13 @@ __global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, Proof
     uint32_t pcw[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)l * 8 + j) * S, lb);
-    const int f = a.f;
-    const int q = f >> 2;
-    const int sh = f & 3;
-    const int nbytes = 20 + a.path_bytes;  // body; the domain byte 0x01 follows
-    const bool cross = f + nbytes >= KECCAK_RATE;
-    const uint32_t amt = (32 - 8 * sh) & 31;
-    const int dw = nbytes >> 2;
-    const uint32_t dbit = 1u << (8 * (nbytes & 3));
     for (int node = nbeg; node < nend; node++) {
-        // body words: seed(4) | le16(BITS) le16(l) | path (<= 8) | 0x01 | zeros
-        uint32_t B[NP_WIN];
+        uint32_t seed[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) B[i] = pld(a.cs + ((size_t)node * 5 + i) * S, lb);
-        B[4] = (uint32_t)p.bits | ((uint32_t)l << 16);
-#pragma unroll
-        for (int k = 5; k < NP_WIN; k++) B[k] = k - 5 < 8 ? a.child_path[node * 8 + (k - 5)] : 0u;
-#pragma unroll
-        for (int k = 4; k < NP_WIN; k++) B[k] |= (k == dw) ? dbit : 0u;
+        for (int i = 0; i < 4; i++) seed[i] = pld(a.cs + ((size_t)node * 5 + i) * S, lb);
         const uint32_t t = pld(a.cs + ((size_t)node * 5 + 4) * S, lb);
-        // shift the window to byte position f % 4
-        uint32_t x[NP_WIN];
-#pragma unroll
-        for (int k = 0; k < NP_WIN; k++) {
-            const uint32_t hi = B[k];
-            const uint32_t lo = k ? B[k - 1] : 0u;
-            x[k] = sh ? __builtin_amdgcn_alignbit(hi, lo, amt) : hi;
-        }
-        asm volatile("" ::: "memory");  // re-read the uniform prefix state, do not pin 50 registers
-        KState s = a.np->st;
-        switch (q) {
-#define NP_W(Q) case Q: np_xor_window<Q>(s, x); break;
-            NP_CASES(NP_W)
-#undef NP_W
-        }
-        if (cross) {
-            keccak_p12(s);
-            switch (q) {
-#define NP_O(Q) case Q: np_xor_overflow<Q>(s, x); break;
-                NP_CASES(NP_O)
-#undef NP_O
-            }
-        }
-        s.a[20].hi ^= 0x80000000u;
-        keccak_p12(s);
-#pragma unroll
-        for (int j = 0; j < 8; j++) pst(a.onehot + ((size_t)node * 8 + j) * S, lb, kword(s, j) ^ (t ? pcw[j] : 0u));
+        node_proof_one(a.np, a.f, p.bits, l, a.path_bytes, seed, a.child_path + node * 8, t, pcw,
+                       [&](int j, uint32_t w) { pst(a.onehot + ((size_t)node * 8 + j) * S, lb, w); });
     }
 }
 
@@ -726,7 +782,16 @@ struct AbsorbArgs {
     const uint32_t* seg[2];
     int nbytes[2];
     int f[2];
+    int prio;  // s_setprio of the sponge waves (0..3)
 };
+MH_D void absorb_setprio(int prio) {
+    switch (prio) {
+        case 0: break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
 
 // The next block's 43 source words are loaded before the current block's
 // permutation, so their HBM/L2 latency hides under ~2.3k VALU instructions.
@@ -736,7 +801,7 @@ struct AbsorbArgs {
 __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     // The sponge chain is the latency-critical path and runs beside the
     // level-eval waves: win every issue arbitration on the shared SIMD.
-    __builtin_amdgcn_s_setprio(3);
+    absorb_setprio(a.prio);
     const int r = blockIdx.x * 256 + threadIdx.x;
     const int which = blockIdx.y;
     if (r >= pl.stride) return;
@@ -812,7 +877,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
 // needs the j = 2i + h, i.e. stream words base + h + k, k < 42, which it loads
 // itself (the plane offset h*S is part of its per-lane buffer offset).
 __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
-    __builtin_amdgcn_s_setprio(3);
+    absorb_setprio(a.prio);
     // (launched with optional dynamic LDS that is never touched: it only caps
     // how many absorb workgroups share a CU, see mastic_ctx::absorb_lds)
     const int h = threadIdx.x & 1;

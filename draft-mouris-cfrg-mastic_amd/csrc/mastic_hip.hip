@@ -93,9 +93,10 @@ struct mastic_ctx {
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
-    bool eval_quad = false;     // 4-block payload refills in k_eval_aes (MASTIC_EVAL_QUAD=1)
+    int proof_waves = EVAL_PROOF_WAVES;  // proof waves per eval workgroup (MASTIC_PROOF_WAVES)
+    int proof_prio = 0;                  // their s_setprio (MASTIC_PROOF_PRIO)
+    int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
-    int eval_dbg = 0;           // timing experiments only (MASTIC_EVAL_DBG, results wrong)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
@@ -506,21 +507,47 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const int wlw = p.value_len * p.w32;
     int f_oh = c->pfx_f[PFX_ONEHOT], f_pl = c->pfx_f[PFX_PAYLOAD];
     auto plane = [&](size_t off) { return W + off * (size_t)stride; };
-    // Three streams per level l:
-    //   stream   k_eval_aes(l)   (LDS-bound AES, 4 waves/SIMD)
-    //   stream3  k_node_proof(l) (VALU-only Keccak) after eval_aes(l)
-    //   stream2  k_absorb(l)     (serial binder sponges) after node_proof(l)
-    // so level l+1's AES overlaps level l's proofs and sponges.  Buffers:
-    // child seeds 2 slots (aes(l) waits node_proof(l-2)), proof / payload
-    // 3 slots (aes(l), node_proof(l) wait absorb(l-3)).
+    // Per level l, on two streams:
+    //   stream   k_eval_aes(l): AES of level l (12 waves per workgroup) and
+    //            the node proofs of level l-1 (4 proof waves per workgroup)
+    //   stream2  k_absorb(l-1): binder sponges over level l-1's proofs and
+    //            payload differences, after eval_aes(l)
+    // so the sponges of one level overlap the evaluation of the next.  The
+    // last level's proofs come from a k_node_proof launch.  Buffers: child
+    // seeds 2 slots; proof / payload 3 slots (eval_aes(l) writes payload(l)
+    // and proofs(l-1), so it waits absorb(l-3)).  Timing: one (eval, proof,
+    // absorb) event triplet per step of the loop below.
     size_t sev = 0;
-    std::vector<hipEvent_t> abs_done(t->L + 1), np_done(t->L + 1);
+    std::vector<hipEvent_t> abs_done(t->L + 1);
+    auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
+        const int slot = lv % NSLOT;
+        AbsorbArgs ab;
+        ab.seg[0] = plane(wl.onehot[slot]);
+        ab.nbytes[0] = 2 * t->n_parents[lv] * 32;
+        ab.f[0] = f_oh;
+        ab.seg[1] = plane(wl.payload[slot]);
+        ab.nbytes[1] = lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
+        ab.f[1] = f_pl;
+        ab.prio = c->absorb_prio;
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, ready, 0));
+        HIPCHK(c, hipEventRecord(e4, c->stream2));
+        if (c->absorb_pair)
+            hipLaunchKernelGGL(k_absorb_pair, dim3((stride + 127) / 128, 2), dim3(256), c->absorb_lds, c->stream2, pl,
+                               ab);
+        else
+            hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
+        HIPCHK(c, hipEventRecord(e5, c->stream2));
+        HIPCHK(c, hipGetLastError());
+        abs_done[lv] = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(abs_done[lv], c->stream2));
+        f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
+        f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
+        return 0;
+    };
     for (int l = 0; l <= t->L; l++) {
         const int slot = l % NSLOT;
         const int np_ = t->n_parents[l];
-        const int nn = 2 * np_;
         if (l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
-        if (l >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, np_done[l - 2], 0));
         AesArgs a;
         a.level = l;
         a.agg_id = agg_id;
@@ -536,73 +563,63 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.payload = plane(wl.payload[slot]);
         a.out = plane(wl.out);
         a.force_slow_blk = c->force_slow_blk;
-        dim3 grid(groups, (np_ + EVAL_WAVES * a.ppw - 1) / (EVAL_WAVES * a.ppw));
+        a.aes_waves = EVAL_WAVES - c->proof_waves;
+        a.proof_prio = c->proof_prio;
+        const int gy = (np_ + a.aes_waves * a.ppw - 1) / (a.aes_waves * a.ppw);
+        a.pv_level = l - 1;
+        a.pv_nodes = l > 0 ? 2 * t->n_parents[l - 1] : 0;
+        a.pv_npw = (a.pv_nodes + gy * c->proof_waves - 1) / (gy * c->proof_waves);
+        a.pv_path_bytes = (l + 7) / 8;
+        a.pv_child_path = l > 0 ? t->d_path.as<uint32_t>() + t->off[l - 1] * 8 : nullptr;
+        a.pv_onehot = l > 0 ? plane(wl.onehot[(l - 1) % NSLOT]) : nullptr;
+        a.np = (const PrefixState*)c->pfx.p + PFX_NODE;
+        a.np_f = c->pfx_f[PFX_NODE];
+        dim3 grid(groups, gy);
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
+        hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
+        hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        bool launched = false;
-        if constexpr (F::W32 == 2) {
-            launched = true;
-            if (c->eval_dbg == 1)
-                hipLaunchKernelGGL((k_eval_aes<F, false, 1>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
-            else if (c->eval_dbg == 3)
-                hipLaunchKernelGGL((k_eval_aes<F, false, 3>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
-            else if (c->eval_dbg == 4)
-                hipLaunchKernelGGL((k_eval_aes<F, false, 4>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
-            else
-                launched = false;
-        }
-        if (launched) {
-        } else if (c->eval_quad)
-            hipLaunchKernelGGL((k_eval_aes<F, true>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
-        else
-            hipLaunchKernelGGL((k_eval_aes<F, false>), grid, dim3(64 * EVAL_WAVES), 0, c->stream, p, pl, a);
+        hipLaunchKernelGGL((k_eval_aes<F, false>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream, p, pl, a);
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(e2, c->stream));
+        HIPCHK(c, hipEventRecord(e3, c->stream));
         hipEvent_t aes_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(aes_done, c->stream));
-
+        if (l > 0) {
+            if (launch_absorb(l - 1, aes_done, e4, e5)) return -1;
+        } else {
+            HIPCHK(c, hipEventRecord(e4, c->stream2));
+            HIPCHK(c, hipEventRecord(e5, c->stream2));
+        }
+    }
+    {
+        // the last level's node proofs, then its sponges
+        const int l = t->L;
+        const int nn = 2 * t->n_parents[l];
         ProofArgs pa;
         pa.level = l;
         pa.n_nodes = nn;
         pa.npw = choose_ppw(nn, groups);
         pa.path_bytes = (l + 1 + 7) / 8;
         pa.child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
-        pa.cs = a.cs_out;
-        pa.onehot = plane(wl.onehot[slot]);
+        pa.cs = plane(wl.cs[l & 1]);
+        pa.onehot = plane(wl.onehot[l % NSLOT]);
         pa.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         pa.f = c->pfx_f[PFX_NODE];
-        HIPCHK(c, hipStreamWaitEvent(c->stream3, aes_done, 0));
-        if (l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream3, abs_done[l - NSLOT], 0));
+        hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
-        HIPCHK(c, hipEventRecord(e2, c->stream3));
-        hipLaunchKernelGGL(k_node_proof, dim3(groups, (nn + 4 * pa.npw - 1) / (4 * pa.npw)), dim3(256), 0,
-                           c->stream3, p, pl, pa);
-        HIPCHK(c, hipEventRecord(e3, c->stream3));
-        HIPCHK(c, hipGetLastError());
-        np_done[l] = get_sync_event(c, sev++);
-        HIPCHK(c, hipEventRecord(np_done[l], c->stream3));
-
-        AbsorbArgs ab;
-        ab.seg[0] = pa.onehot;
-        ab.nbytes[0] = nn * 32;
-        ab.f[0] = f_oh;
-        ab.seg[1] = a.payload;
-        ab.nbytes[1] = l > 0 ? np_ * wlw * 4 : 0;
-        ab.f[1] = f_pl;
-        HIPCHK(c, hipStreamWaitEvent(c->stream2, np_done[l], 0));
         hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
-        HIPCHK(c, hipEventRecord(e4, c->stream2));
-        if (c->absorb_pair)
-            hipLaunchKernelGGL(k_absorb_pair, dim3((stride + 127) / 128, 2), dim3(256), c->absorb_lds, c->stream2, pl,
-                               ab);
-        else
-            hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
-        HIPCHK(c, hipEventRecord(e5, c->stream2));
+        HIPCHK(c, hipEventRecord(e0, c->stream));
+        HIPCHK(c, hipEventRecord(e1, c->stream));
+        HIPCHK(c, hipEventRecord(e2, c->stream));
+        hipLaunchKernelGGL(k_node_proof, dim3(groups, (nn + 4 * pa.npw - 1) / (4 * pa.npw)), dim3(256), 0,
+                           c->stream, p, pl, pa);
+        HIPCHK(c, hipEventRecord(e3, c->stream));
         HIPCHK(c, hipGetLastError());
-        abs_done[l] = get_sync_event(c, sev++);
-        HIPCHK(c, hipEventRecord(abs_done[l], c->stream2));
-        f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
-        f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
+        hipEvent_t np_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(np_done, c->stream));
+        if (launch_absorb(l, np_done, e4, e5)) return -1;
     }
     HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
@@ -1121,12 +1138,23 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         c->absorb_pair = !(e && e[0] == '1');
         const char* l = getenv("MASTIC_ABSORB_LDS_KB");
         c->absorb_lds = l ? std::max(0, std::min(64, atoi(l))) * 1024 : 0;
-        const char* q = getenv("MASTIC_EVAL_QUAD");
-        c->eval_quad = q && q[0] == '1';
-        const char* dbg = getenv("MASTIC_EVAL_DBG");
-        c->eval_dbg = dbg ? atoi(dbg) : 0;
+        const char* pw = getenv("MASTIC_PROOF_WAVES");
+        if (pw) c->proof_waves = std::max(1, std::min(8, atoi(pw)));
+        const char* ap = getenv("MASTIC_ABSORB_PRIO");
+        if (ap) c->absorb_prio = std::max(0, std::min(3, atoi(ap)));
+        const char* pp = getenv("MASTIC_PROOF_PRIO");
+        if (pp) c->proof_prio = std::max(0, std::min(2, atoi(pp)));
         const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
         c->force_slow_blk = fs ? atoi(fs) : -1;
+    }
+    // the level kernel's LDS (table + key schedules) is dynamic, above the
+    // 64 KiB default
+    if (hipFuncSetAttribute((const void*)k_eval_aes<F64, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            EVAL_LDS_BYTES) != hipSuccess) {
+        delete c;
+        return MASTIC_EHIP;
     }
     // the binder sponges are the latency-critical chain: their stream gets the
     // highest priority so their workgroups are dispatched first

@@ -128,7 +128,9 @@ void run(uint32_t* out, int wg_per_cu, const char* name) {
     fflush(stdout);
 }
 
+int main_ladder();
 int main() {
+    if (main_ladder()) return 1;
     uint32_t* out;
     hipMalloc(&out, 256 * 16 * 1024 * 4 * sizeof(uint32_t));
     run<0, 1, 16>(out, 1, "perm64K nb1 w16");
@@ -143,6 +145,120 @@ int main() {
     run<1, 4, 8>(out, 3, "t0_32K nb4 w8 (3 wg/cu)");
     run<1, 2, 16>(out, 2, "t0_32K nb2 w16 (2 wg/cu)");
     run<1, 4, 16>(out, 2, "t0_32K nb4 w16 (2 wg/cu)");
+    hipFree(out);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Level-kernel ladder: the real kernel's per-parent structure (extend pair ->
+// seed pair -> 9 payload pairs), 16 waves per workgroup, 64 reports per
+// workgroup, planes [word][stride] in HBM like the product.
+//   FLAGS & 1: store child seeds (10 words) + payload diff (34) + frontier (68)
+//   FLAGS & 2: load parent seed (5 words) + parent payload (34)
+template <int FLAGS>
+__global__ __launch_bounds__(1024) void k_ladder(uint32_t* planes, int stride, int parents_per_wave, uint32_t* out) {
+    __shared__ uint32_t T[AES_PERM_LDS_WORDS];
+    __shared__ uint4 RKE[64 * 11];
+    __shared__ uint4 RKC[64 * 11];
+    aes_perm_fill(T, threadIdx.x, 1024);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int i = threadIdx.x; i < 64 * 44; i += 1024) {
+        const uint32_t v = 0x9e3779b9u * (uint32_t)(i + 1) ^ (blockIdx.x << 7);
+        ((uint32_t*)RKE)[i] = aes_perm_key_word(i % 44, v);
+        ((uint32_t*)RKC)[i] = aes_perm_key_word(i % 44, v * 3u);
+    }
+    __syncthreads();
+    const AesPerm TL{T, 4u * (uint32_t)(lane & 31), 128u + 4u * (uint32_t)(lane & 31)};
+    const RkLds rke{RKE + lane * 11};
+    const RkLds rkc{RKC + lane * 11};
+    const int r = blockIdx.x * 64 + lane;
+    const uint32_t lb = (uint32_t)r * 4u;
+    const int S = stride;
+    uint32_t acc = 0;
+    const int p0 = (blockIdx.y * 16 + wave) * parents_per_wave;
+    for (int pi = p0; pi < p0 + parents_per_wave; pi++) {
+        asm volatile("" ::: "memory");
+        uint32_t ps[4];
+        if (FLAGS & 2) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) ps[i] = pld(planes + ((size_t)pi * 5 + i) * S, lb);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) ps[i] = pi * 4 + i + lane;
+        }
+        uint32_t cs0[4], cs1[4], ns0[4], ns1[4];
+        fixed_key_block2(TL, rke, ps, 0u, ps, 1u, cs0, cs1);
+        cs0[0] &= ~1u;
+        cs1[0] &= ~1u;
+        fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
+        if (FLAGS & 1) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                pst(planes + ((size_t)(2 * pi) * 5 + i) * S, lb, ns0[i]);
+                pst(planes + ((size_t)(2 * pi + 1) * 5 + i) * S, lb, ns1[i]);
+            }
+        } else {
+            acc ^= ns0[0] ^ ns1[1];
+        }
+        for (int b = 0; b < 9; b++) {
+            asm volatile("" ::: "memory");
+            uint32_t wp[4];
+            if (FLAGS & 2) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) wp[i] = pld(planes + ((size_t)pi * 36 + 4 * b + i) * S, lb);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++) wp[i] = b + i;
+            }
+            uint32_t o0[4], o1[4];
+            fixed_key_block2(TL, rkc, cs0, (uint32_t)(b + 1), cs1, (uint32_t)(b + 1), o0, o1);
+            if (FLAGS & 1) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    pst(planes + ((size_t)(2 * pi) * 36 + 4 * b + i) * S, lb, o0[i]);
+                    pst(planes + ((size_t)(2 * pi + 1) * 36 + 4 * b + i) * S, lb, o1[i]);
+                    pst(planes + ((size_t)pi * 36 + 4 * b + i + 7) * S, lb, wp[i] - o0[i] - o1[i]);
+                }
+            } else {
+                acc ^= o0[0] ^ o1[1] ^ o0[2] ^ o1[3] ^ wp[0];
+            }
+        }
+    }
+    out[blockIdx.y * gridDim.x * 1024 + blockIdx.x * 1024 + threadIdx.x] = acc;
+}
+
+template <int FLAGS>
+void run_ladder(uint32_t* planes, int stride, uint32_t* out, const char* name) {
+    const int groups = stride / 64, ppw = 32, ychunks = 10;  // 10 * 16 * 32 = 5120 parents
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_ladder<FLAGS>), dim3(groups, 1), dim3(1024), 0, 0, planes, stride, 1, out);
+    hipDeviceSynchronize();
+    hipEventRecord(a);
+    hipLaunchKernelGGL((k_ladder<FLAGS>), dim3(groups, ychunks), dim3(1024), 0, 0, planes, stride, ppw, out);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    const double blocks = (double)stride * ychunks * 16 * ppw * 22;
+    printf("{\"variant\": \"ladder %s\", \"ms\": %.3f, \"blocks_per_s\": %.4g}\n", name, ms, blocks / (ms / 1e3));
+    fflush(stdout);
+}
+
+int main_ladder() {
+    const int stride = 4096;
+    uint32_t *planes, *out;
+    const size_t words = (size_t)5120 * 2 * 36 + 64;
+    if (hipMalloc(&planes, words * stride * 4) != hipSuccess) return 1;
+    hipMemset(planes, 0, words * stride * 4);
+    hipMalloc(&out, (size_t)10 * (stride / 64) * 1024 * 4);
+    run_ladder<0>(planes, stride, out, "compute only");
+    run_ladder<1>(planes, stride, out, "+stores");
+    run_ladder<2>(planes, stride, out, "+loads");
+    run_ladder<3>(planes, stride, out, "+loads+stores");
+    hipFree(planes);
     hipFree(out);
     return 0;
 }
