@@ -494,7 +494,9 @@ struct AesArgs {
     int pv_npw;                     // nodes per proof wave
     int pv_path_bytes;              // ceil(level / 8)
     const uint32_t* pv_child_path;  // [pv_nodes][8]
-    uint32_t* pv_onehot;            // [pv_nodes * 8] proof planes of level - 1
+    uint32_t* pv_onehot;            // [pv_nodes * 8] proofs of level - 1 (tiled, see AbsorbArgs)
+    int oh_gstride;                 // words per report group of the proof buffers
+    int pay_gstride;                // ... of the payload-difference buffers
     const PrefixState* np;          // node-proof prefix state
     int np_f;                       // its fill position
     int aes_waves;                  // waves [0, aes_waves) walk parents, the rest are proof waves
@@ -562,6 +564,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         if (nbeg >= a.pv_nodes) return;
         const int nend = min(nbeg + a.pv_npw, a.pv_nodes);
         const int pl_ = a.pv_level;
+        uint32_t* ohg = a.pv_onehot + (size_t)blockIdx.x * a.oh_gstride;  // tile group of these 64 reports
+        const uint32_t lt = (uint32_t)lane * 4u;
         uint32_t pcw[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)pl_ * 8 + j) * S, lb);
@@ -571,7 +575,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_in + ((size_t)node * 5 + i) * S, lb);
             const uint32_t t = pld(a.cs_in + ((size_t)node * 5 + 4) * S, lb);
             node_proof_one(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
-                           [&](int j, uint32_t w) { pst(a.pv_onehot + ((size_t)node * 8 + j) * S, lb, w); });
+                           [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * 64, lt, w); });
         }
         return;
     }
@@ -647,6 +651,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         // Element e of both children: payload correction, frontier payloads,
         // the parent's payload difference (or the root sum), out shares.
+        uint32_t* const payg = a.payload + (size_t)blockIdx.x * a.pay_gstride;  // tiled group
         auto emit = [&](int e, E x0, E x1, E cw, E wp) {
             if (tc0) x0 = F::add(x0, cw);
             if (tc1) x1 = F::add(x1, cw);
@@ -655,7 +660,11 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             if (l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
-                pl_store<F>(a.payload, pi * vl + e, S, r, F::sub(F::sub(wp, x0), x1));
+                // tiled (AbsorbArgs): word m of this group's 64 reports = one row
+                const E d = F::sub(F::sub(wp, x0), x1);
+#pragma unroll
+                for (int i = 0; i < F::W32; i++)
+                    pst(payg + ((size_t)(pi * vl + e) * F::W32 + i) * 64, (uint32_t)lane * 4u, F::word(d, i));
             }
             if (pf0 >= 0 || pf1 >= 0) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
@@ -741,6 +750,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 // lands at the uniform fill position f: a switch on f/4 selects a straight-
 // line XOR pattern, so no LDS staging and no per-lane indexing is needed.
 struct ProofArgs {
+    int oh_gstride;      // words per report group of the (tiled) proof buffer
     int level;
     int n_nodes;
     int npw;             // nodes per wave
@@ -762,6 +772,8 @@ __global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, Proof
     if (nbeg >= a.n_nodes) return;
     const int nend = min(nbeg + a.npw, a.n_nodes);
     const int l = a.level;
+    uint32_t* ohg = a.onehot + (size_t)blockIdx.x * a.oh_gstride;  // tiled proof buffer of this group
+    const uint32_t lt = (uint32_t)lane * 4u;
     uint32_t pcw[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)l * 8 + j) * S, lb);
@@ -771,15 +783,21 @@ __global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, Proof
         for (int i = 0; i < 4; i++) seed[i] = pld(a.cs + ((size_t)node * 5 + i) * S, lb);
         const uint32_t t = pld(a.cs + ((size_t)node * 5 + 4) * S, lb);
         node_proof_one(a.np, a.f, p.bits, l, a.path_bytes, seed, a.child_path + node * 8, t, pcw,
-                       [&](int j, uint32_t w) { pst(a.onehot + ((size_t)node * 8 + j) * S, lb, w); });
+                       [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * 64, lt, w); });
     }
 }
 
 // ------------------------------------------------------------- binder absorb
 // Continues the one-hot (sponge 0) or payload (sponge 1) TurboSHAKE over the
 // words one level produced.  Positions are uniform (tracked by the host).
+// Level buffers (proofs, payload differences) are TILED, not planes: word m
+// of report r sits at  seg + (r / 64) * gstride + m * 64 + r % 64,  so a
+// sponge wave (one report group) streams one contiguous region block after
+// block, and a level-kernel store of one word for 64 reports is still one
+// 256-byte row.
 struct AbsorbArgs {
     const uint32_t* seg[2];
+    int gstride[2];  // words per report group of each tiled segment
     int nbytes[2];
     int f[2];
     int prio;  // s_setprio of the sponge waves (0..3)
@@ -809,8 +827,9 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     if (nb == 0) return;
     const int S = pl.stride;
     uint32_t* sp = which == 0 ? pl.sp_onehot : pl.sp_payload;
-    const uint32_t* seg = a.seg[which];
+    const uint32_t* seg = a.seg[which] + (size_t)(r >> 6) * a.gstride[which];  // this wave's tile group
     const uint32_t lb = (uint32_t)r * 4u;
+    const uint32_t lt = (uint32_t)(r & 63) * 4u;  // lane offset inside a tile row
     KState s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = u32x2{pld(sp + (size_t)(2 * i) * S, lb), pld(sp + (size_t)(2 * i + 1) * S, lb)};
@@ -821,19 +840,18 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     const int amt = (32 - 8 * sh) & 31;  // block word j = alignbit(w[j+1], w[j], amt)
     const int nw = (nb + 3) >> 2;
     const int end = f + nb;
-    const uint32_t pstride = (uint32_t)S * 4u;
     auto load_block = [&](int b, uint32_t* w) {
         const int base = KECCAK_RATE_WORDS * b - q - off;
         if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
-            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * S);
-            // the plane offset is a running SGPR sum made opaque at every step,
+            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * 64);
+            // the row offset is a running SGPR sum made opaque at every step,
             // so the compiler cannot hoist 43 loop-invariant offsets (which it
             // would spill to VGPRs and then waterfall)
             uint32_t so = 0;
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
-                w[j] = pld_so(rs, lb, so);
-                so += pstride;
+                w[j] = pld_so(rs, lt, so);
+                so += 256u;
                 asm volatile("" : "+s"(so));
             }
         } else {
@@ -841,7 +859,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
                 const int m = base + j;
                 const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-                w[j] = pld(seg + (size_t)mc * S, lb);
+                w[j] = pld(seg + (size_t)mc * 64, lt);
             }
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
@@ -850,20 +868,19 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
             }
         }
     };
+    // one block buffer, next block's loads issued after the XOR (see k_absorb_pair)
     uint32_t cur[KECCAK_RATE_WORDS + 1];
     load_block(0, cur);
     for (int b = 0;; b++) {
         const bool full = end >= KECCAK_RATE * (b + 1);
         const bool more = end > KECCAK_RATE * (b + 1);
-        uint32_t nxt[KECCAK_RATE_WORDS + 1];
-        if (more) load_block(b + 1, nxt);
 #pragma unroll
         for (int j = 0; j < KECCAK_RATE_WORDS; j++) kxor_word(s, j, __builtin_amdgcn_alignbit(cur[j + 1], cur[j], amt));
         if (!full) break;
+        asm volatile("" ::: "memory");
+        if (more) load_block(b + 1, cur);
         keccak_p12(s);
         if (!more) break;
-#pragma unroll
-        for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) cur[j] = nxt[j];
     }
 #pragma unroll
     for (int i = 0; i < 25; i++) {
@@ -888,9 +905,10 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     if (nb == 0) return;
     const int S = pl.stride;
     uint32_t* sp = which == 0 ? pl.sp_onehot : pl.sp_payload;
-    const uint32_t* seg = a.seg[which];
-    const uint32_t lb = (uint32_t)r * 4u;
-    const uint32_t lbh = ((uint32_t)h * (uint32_t)S + (uint32_t)r) * 4u;  // plane h of the pair
+    const uint32_t* seg = a.seg[which] + (size_t)(r >> 6) * a.gstride[which];  // this wave's tile group
+    const uint32_t lbh = ((uint32_t)h * (uint32_t)S + (uint32_t)r) * 4u;  // state plane h of the pair
+    const uint32_t lt = (uint32_t)(r & 63) * 4u;                            // lane offset in a tile row
+    const uint32_t lth = lt + (uint32_t)h * 256u;                           // ... of the next row for h = 1
     KHalf s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = pld(sp + (size_t)(2 * i) * S, lbh);
@@ -902,16 +920,15 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     const int nw = (nb + 3) >> 2;
     const int end = f + nb;
     constexpr int NL = KECCAK_RATE_WORDS;  // words loaded per lane and block
-    const uint32_t pstride = (uint32_t)S * 4u;
     auto load_block = [&](int b, uint32_t* w) {
         const int base = KECCAK_RATE_WORDS * b - q - off;
         if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
-            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * S);
-            uint32_t so = 0;  // running opaque plane offset, as in k_absorb
+            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * 64);
+            uint32_t so = 0;  // running opaque row offset, as in k_absorb
 #pragma unroll
             for (int k = 0; k < NL; k++) {
-                w[k] = pld_so(rs, lbh, so);
-                so += pstride;
+                w[k] = pld_so(rs, lth, so);
+                so += 256u;
                 asm volatile("" : "+s"(so));
             }
         } else {
@@ -923,7 +940,7 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
             for (int k = 0; k < NL + 1; k++) {
                 const int m = base + k;
                 const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-                t[k] = pld(seg + (size_t)mc * S, lb);
+                t[k] = pld(seg + (size_t)mc * 64, lt);
             }
 #pragma unroll
             for (int k = 0; k < NL + 1; k++) {
@@ -934,20 +951,24 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
             for (int k = 0; k < NL; k++) w[k] = h ? t[k + 1] : t[k];
         }
     };
+    // One block buffer.  Per block: XOR the current block (waits for its
+    // loads), THEN issue the next block's loads into the same registers, then
+    // permute: the loads in flight during the permutation are exactly the
+    // ones the next XOR waits for (vmcnt counts in issue order; loads issued
+    // before the XOR would make its wait drain them too and expose the whole
+    // memory latency once per block).
     uint32_t cur[NL];
     load_block(0, cur);
     for (int b = 0;; b++) {
         const bool full = end >= KECCAK_RATE * (b + 1);
         const bool more = end > KECCAK_RATE * (b + 1);
-        uint32_t nxt[NL];
-        if (more) load_block(b + 1, nxt);
 #pragma unroll
         for (int i = 0; i < 21; i++) s.a[i] ^= __builtin_amdgcn_alignbit(cur[2 * i + 1], cur[2 * i], amt);
         if (!full) break;
+        asm volatile("" ::: "memory");
+        if (more) load_block(b + 1, cur);
         keccak_p12_pair(s, h != 0);
         if (!more) break;
-#pragma unroll
-        for (int k = 0; k < NL; k++) cur[k] = nxt[k];
     }
 #pragma unroll
     for (int i = 0; i < 25; i++) pst(sp + (size_t)(2 * i) * S, lbh, s.a[i]);

@@ -95,6 +95,7 @@ struct mastic_ctx {
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
     int proof_waves = EVAL_PROOF_WAVES;  // proof waves per eval workgroup (MASTIC_PROOF_WAVES)
     int proof_prio = 0;                  // their s_setprio (MASTIC_PROOF_PRIO)
+    int stride_pad = 64;                 // words of padding per plane row (MASTIC_STRIDE_PAD)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
@@ -503,7 +504,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     hipLaunchKernelGGL(k_setup, dim3((stride + 255) / 256), dim3(256), 0, c->stream, pl, pfx);
     HIPCHK(c, hipGetLastError());
 
-    const int groups = stride / 64;
+    const int groups = (n + 63) / 64;  // report groups (rows beyond n are padding)
     const int wlw = p.value_len * p.w32;
     int f_oh = c->pfx_f[PFX_ONEHOT], f_pl = c->pfx_f[PFX_PAYLOAD];
     auto plane = [&](size_t off) { return W + off * (size_t)stride; };
@@ -519,23 +520,28 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // absorb) event triplet per step of the loop below.
     size_t sev = 0;
     std::vector<hipEvent_t> abs_done(t->L + 1);
+    // tiled level buffers (kernels.hpp AbsorbArgs): words per report group
+    const int oh_gstride = t->max_level_nodes * 8 * 64;
+    const int pay_gstride = t->max_parents * wlw * 64;
     auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
         const int slot = lv % NSLOT;
         AbsorbArgs ab;
         ab.seg[0] = plane(wl.onehot[slot]);
+        ab.gstride[0] = oh_gstride;
         ab.nbytes[0] = 2 * t->n_parents[lv] * 32;
         ab.f[0] = f_oh;
         ab.seg[1] = plane(wl.payload[slot]);
+        ab.gstride[1] = pay_gstride;
         ab.nbytes[1] = lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
         ab.f[1] = f_pl;
         ab.prio = c->absorb_prio;
         HIPCHK(c, hipStreamWaitEvent(c->stream2, ready, 0));
         HIPCHK(c, hipEventRecord(e4, c->stream2));
         if (c->absorb_pair)
-            hipLaunchKernelGGL(k_absorb_pair, dim3((stride + 127) / 128, 2), dim3(256), c->absorb_lds, c->stream2, pl,
-                               ab);
+            hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 + 127) / 128, 2), dim3(256), c->absorb_lds,
+                               c->stream2, pl, ab);
         else
-            hipLaunchKernelGGL(k_absorb, dim3((stride + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
+            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
         HIPCHK(c, hipEventRecord(e5, c->stream2));
         HIPCHK(c, hipGetLastError());
         abs_done[lv] = get_sync_event(c, sev++);
@@ -572,6 +578,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.pv_path_bytes = (l + 7) / 8;
         a.pv_child_path = l > 0 ? t->d_path.as<uint32_t>() + t->off[l - 1] * 8 : nullptr;
         a.pv_onehot = l > 0 ? plane(wl.onehot[(l - 1) % NSLOT]) : nullptr;
+        a.oh_gstride = oh_gstride;
+        a.pay_gstride = pay_gstride;
         a.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         a.np_f = c->pfx_f[PFX_NODE];
         dim3 grid(groups, gy);
@@ -605,6 +613,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         pa.child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
         pa.cs = plane(wl.cs[l & 1]);
         pa.onehot = plane(wl.onehot[l % NSLOT]);
+        pa.oh_gstride = oh_gstride;
         pa.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         pa.f = c->pfx_f[PFX_NODE];
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
@@ -652,7 +661,9 @@ static uint64_t default_budget(mastic_ctx* c) {
     if (c->budget) return c->budget;
     size_t freeb = 0, total = 0;
     if (hipMemGetInfo(&freeb, &total) != hipSuccess) return 1ull << 30;
-    return (uint64_t)(freeb * 0.45);
+    // work buffers are the only large allocation (C2: ~8.6 MB per report);
+    // one chunk per batch keeps one binder-sponge chain per prep_init
+    return (uint64_t)(freeb * 0.75);
 }
 
 extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_t verify_key[32],
@@ -691,16 +702,23 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     }
     const uint64_t budget = default_budget(c);
     const size_t per_report = wl.words * 4;
-    size_t chunk = std::min<size_t>(round_up(n, 64), (budget / per_report) / 64 * 64);
+    // Plane rows are padded by stride_pad words: with a power-of-two row
+    // length every word of a report sits at the same address bits modulo a
+    // large power of two, and the 42-plane block loads of the binder sponges
+    // all land on the same memory channels.
+    const size_t pad = (size_t)c->stride_pad;
+    size_t by_budget = (budget / per_report) / 64 * 64;
+    if (by_budget > pad + 64) by_budget -= pad;  // the padded rows count against the budget too
+    size_t chunk = std::min<size_t>(round_up(n, 64), by_budget);
     if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
-    if (!c->work.ensure(per_report * chunk))
-        return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * chunk);
+    if (!c->work.ensure(per_report * (chunk + pad)))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * (chunk + pad));
     size_t evi = 0;
     hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
     HIPCHK(c, hipEventRecord(t0, c->stream));
     for (size_t b = 0; b < n; b += chunk) {
         const int nn = (int)std::min(chunk, n - b);
-        const int stride = (int)round_up(nn, 64);
+        const int stride = (int)(round_up(nn, 64) + pad);
         rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi)
                            : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi);
         if (rc) return rc;
@@ -1137,9 +1155,11 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         const char* e = getenv("MASTIC_ABSORB_SINGLE");
         c->absorb_pair = !(e && e[0] == '1');
         const char* l = getenv("MASTIC_ABSORB_LDS_KB");
-        c->absorb_lds = l ? std::max(0, std::min(64, atoi(l))) * 1024 : 0;
+        c->absorb_lds = l ? std::max(0, std::min(160, atoi(l))) * 1024 : 0;
         const char* pw = getenv("MASTIC_PROOF_WAVES");
         if (pw) c->proof_waves = std::max(1, std::min(8, atoi(pw)));
+        const char* spd = getenv("MASTIC_STRIDE_PAD");
+        if (spd) c->stride_pad = std::max(0, std::min(1 << 20, atoi(spd))) / 64 * 64;
         const char* ap = getenv("MASTIC_ABSORB_PRIO");
         if (ap) c->absorb_prio = std::max(0, std::min(3, atoi(ap)));
         const char* pp = getenv("MASTIC_PROOF_PRIO");
@@ -1152,7 +1172,9 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     if (hipFuncSetAttribute((const void*)k_eval_aes<F64, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_eval_aes<F128, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            EVAL_LDS_BYTES) != hipSuccess) {
+                            EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_absorb_pair, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess) {
         delete c;
         return MASTIC_EHIP;
     }

@@ -337,14 +337,16 @@ def test_c2_shape_properties_and_oracle_sample(mastic_amd):
     for (a, w) in zip(alphas, weights):
         want[a] = want.get(a, 0) + w
     assert result == [want.get(p, 0) for p in ap[1]]
-    # one report through the oracle at full size
+    # reports of both 64-report groups through the oracle at full size (the
+    # binder buffers are tiled per report group)
     o = _oracle_for(m)
-    i = 0
-    cws = o.vidpf.decode_public_share(pub[:m.public_share_size()])
-    isd = o.decode_input_share(1, in1[:m.input_share_size(1)])
-    (_st, sh) = o.prep_init(vk, CTX, 1, ap, nonces[:16], cws, isd)
-    enc = o.test_vec_encode_prep_share(sh)
-    assert res[1][0][:len(enc)] == enc
+    psz, isz = m.public_share_size(), m.input_share_size(1)
+    for i in (0, 100):
+        cws = o.vidpf.decode_public_share(pub[psz * i:psz * (i + 1)])
+        isd = o.decode_input_share(1, in1[isz * i:isz * (i + 1)])
+        (_st, sh) = o.prep_init(vk, CTX, 1, ap, nonces[16 * i:16 * (i + 1)], cws, isd)
+        enc = o.test_vec_encode_prep_share(sh)
+        assert res[1][0][len(enc) * i:len(enc) * (i + 1)] == enc, "report %d" % i
 
 
 @pytest.mark.parametrize("blk", [0, 1, 4, 8])
