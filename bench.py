@@ -162,16 +162,16 @@ def main():
 
     units = args.reports * len(attrs) * args.steps * world
     value = units / dt
-    # roofline of the dominant kernel: algorithmic int32 ops (fixed convention)
+    # roofline of the dominant kernel: algorithmic int32 ops (fixed convention).
+    # k_eval_aes runs each level's AES (extend, convert: 1 + ceil(VL*ENC/16) blocks, payload
+    # adds) and, in its proof waves, the previous level's node proofs (one Keccak-p per node);
+    # the last level's proofs run in k_node_proof, so the pair is timed together.
     aes_per_node = 1 + (16 + m.VALUE_LEN * m.field.ENCODED_SIZE + 15) // 16
     aes_ops_node = aes_per_node * AES_BLOCK_OPS + 2 * m.VALUE_LEN * F64_ADD_OPS
     node_units = nodes * args.reports * args.steps
-    kern = {
-        "k_eval_aes<F64>": (aes_ms, aes_ops_node),
-        "k_node_proof": (proof_ms, KECCAK_OPS),
-    }
-    dom = max(kern, key=lambda k: kern[k][0])
-    (dom_ms, dom_ops) = kern[dom]
+    dom = "k_eval_aes<F64> (+ node-proof waves, + k_node_proof for the last level)"
+    dom_ms = aes_ms + proof_ms
+    dom_ops = aes_ops_node + KECCAK_OPS
     achieved = node_units * dom_ops / (dom_ms / 1e3) / 1e12 if dom_ms > 0 else 0.0
     # binder sponges: one-hot 32 B/node, payload VL*ENC B/interior node
     absorb_perms = (32 * nodes + m.VALUE_LEN * m.field.ENCODED_SIZE * interior) / 168.0
@@ -211,13 +211,11 @@ def main():
         },
         "breakdown_ms_per_step": {
             "eval_aes": aes_ms / args.steps,
-            "node_proof": proof_ms / args.steps,
+            "node_proof_last_level": proof_ms / args.steps,
             "absorb": absorb_ms / args.steps,
             "prep_init_total": total_ms / args.steps,
-            "frac_int_valu_eval_aes": (node_units * aes_ops_node / (aes_ms / 1e3) / 1e12 / VALU_PEAK_TOPS)
-            if aes_ms > 0 else None,
-            "frac_int_valu_node_proof": (node_units * KECCAK_OPS / (proof_ms / 1e3) / 1e12 / VALU_PEAK_TOPS)
-            if proof_ms > 0 else None,
+            "frac_int_valu_whole_step": (node_units * (aes_ops_node + KECCAK_OPS) + absorb_perms * args.reports *
+                                         args.steps * KECCAK_OPS) / (dt * 1e12) / VALU_PEAK_TOPS,
             "absorb_keccak_perms_per_report": absorb_perms,
         },
     }
