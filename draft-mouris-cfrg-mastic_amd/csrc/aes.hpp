@@ -209,23 +209,43 @@ MH_D void fixed_key_block2(const TT& T, const RK& rk, const uint32_t sa[4], uint
 //   T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = T0[a] ^ T2[c] ^ rot8(T0[b] ^ T2[d]).
 // A round costs 16 v_perm + 4 x (xor3, rot, xor3) = 28 VALU against
 // 52 with one rotated table and two-instruction addressing.
-#define AES_PERM_LDS_WORDS (256 * 64)
+//
+// AES_T4 (default): all four tables.  A second 64 KiB block at LDS address
+// 64 KiB holds T1 = rot8(T0) and T3 = rot24(T0) in the same layout; its lane
+// byte register carries 0x01 in byte 2, which the v_perm selector copies into
+// address bits 16..23, so every lookup is still ONE v_perm.  A column is then
+// two xor3 (T0 ^ T1 ^ T2, then ^ T3 ^ k): 16 v_perm + 8 VALU per round (24
+// instead of 28), plain round keys, 128 KiB of LDS.
+#ifndef AES_T4
+#define AES_T4 1
+#endif
+#define AES_PERM_LDS_WORDS (AES_T4 ? 256 * 128 : 256 * 64)
 
 MH_D void aes_perm_fill(uint32_t* T, int tid, int nthreads) {
     for (int i = tid; i < AES_PERM_LDS_WORDS; i += nthreads) {
-        const uint32_t t0 = aes_t0(i >> 6);
-        T[i] = (i & 32) ? rot16(t0) : t0;
+        const uint32_t t0 = aes_t0((i >> 6) & 255);
+        const bool hi = i >= 256 * 64;  // T1 / T3 block
+        T[i] = (i & 32) ? (hi ? rot24(t0) : rot16(t0)) : (hi ? rot8(t0) : t0);
     }
 }
 
 struct AesPerm {
-    const uint32_t* T;  // the 64 KiB table; must sit at LDS address 0 (see lookup_n)
+    const uint32_t* T;  // the table; must sit at LDS address 0 (see lds_read_asm)
     uint32_t lb0;       // 4 * (lane & 31)
     uint32_t lb2;       // 128 + 4 * (lane & 31)
     template <int K>
     MH_D uint32_t a0(uint32_t x) const { return __builtin_amdgcn_perm(x, lb0, 0x0c0c0000u | ((4u + K) << 8)); }
     template <int K>
     MH_D uint32_t a2(uint32_t x) const { return __builtin_amdgcn_perm(x, lb2, 0x0c0c0000u | ((4u + K) << 8)); }
+    // T1 / T3 (AES_T4): same lane bytes plus 0x01 in byte 2 -> +64 KiB
+    template <int K>
+    MH_D uint32_t a1(uint32_t x) const {
+        return __builtin_amdgcn_perm(x, lb0 | 0x10000u, 0x0c020000u | ((4u + K) << 8));
+    }
+    template <int K>
+    MH_D uint32_t a3(uint32_t x) const {
+        return __builtin_amdgcn_perm(x, lb2 | 0x10000u, 0x0c020000u | ((4u + K) << 8));
+    }
     template <int K>
     MH_D uint32_t t0(uint32_t x) const { return *(const uint32_t*)((const char*)T + a0<K>(x)); }
     template <int K>
@@ -243,26 +263,13 @@ MH_D uint32_t lds_read_asm(uint32_t a) {
     return v;
 }
 
-// One full round column: T0[b0(w0)] ^ T1[b1(w1)] ^ T2[b2(w2)] ^ T3[b3(w3)] ^ k,
-// given kr = rotr8(k):  T0[.] ^ T2[.] ^ rot8(T0[.] ^ T2[.] ^ kr)  — three VALU
-// after the four lookups.  Key schedules used with AesPerm therefore hold
-// rounds 1..9 rotated right by 8 (aes_perm_key_word); rounds 0 and 10 plain.
-MH_D uint32_t aes_col(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t kr) {
-    const uint32_t r = rot8(xor3_u32(T.t0<1>(w1), T.t2<3>(w3), kr));
-    return xor3_u32(T.t0<0>(w0), T.t2<2>(w2), r);
-}
-// Word i (< 44) of a key schedule as stored for AesPerm.
+// Word i (< 44) of a key schedule as stored for AesPerm: plain with AES_T4;
+// with two tables a column is T0[.] ^ T2[.] ^ rot8(T0[.] ^ T2[.] ^ rotr8(k)),
+// so rounds 1..9 are stored rotated right by 8.
 MH_HD uint32_t aes_perm_key_word(int i, uint32_t w) {
+    if (AES_T4) return w;
     return (i >= 4 && i < 40) ? ((w >> 8) | (w << 24)) : w;
 }
-// Final-round column: S-box bytes (byte 1 of the T0 entries) packed with two
-// v_perm_b32 and merged with the round key by one xor3.
-MH_D uint32_t aes_col_last(const AesPerm& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t k) {
-    const uint32_t lo = __builtin_amdgcn_perm(T.t0<1>(w1), T.t0<0>(w0), 0x0c0c0501u);
-    const uint32_t hi = __builtin_amdgcn_perm(T.t0<3>(w3), T.t0<2>(w2), 0x05010c0cu);
-    return xor3_u32(lo, hi, k);
-}
-
 // Middle rounds.  All 16 N table lookups of a round are issued before any is
 // consumed: an empty asm statement takes every lookup result as an operand,
 // so the compiler cannot interleave "two reads, wait, xor" (which it does
@@ -296,9 +303,9 @@ MH_D void aes_round_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             L[16 * j + 4 * c + 0] = lds_read_asm(T.a0<0>(s[j][c]));
-            L[16 * j + 4 * c + 1] = lds_read_asm(T.a0<1>(s[j][(c + 1) & 3]));
+            L[16 * j + 4 * c + 1] = lds_read_asm(AES_T4 ? T.a1<1>(s[j][(c + 1) & 3]) : T.a0<1>(s[j][(c + 1) & 3]));
             L[16 * j + 4 * c + 2] = lds_read_asm(T.a2<2>(s[j][(c + 2) & 3]));
-            L[16 * j + 4 * c + 3] = lds_read_asm(T.a2<3>(s[j][(c + 3) & 3]));
+            L[16 * j + 4 * c + 3] = lds_read_asm(AES_T4 ? T.a3<3>(s[j][(c + 3) & 3]) : T.a2<3>(s[j][(c + 3) & 3]));
         }
     aes_pin<N>(L);
     const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
@@ -307,7 +314,10 @@ MH_D void aes_round_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const uint32_t* q = L + 16 * j + 4 * c;
-            s[j][c] = xor3_u32(q[0], q[2], rot8(xor3_u32(q[1], q[3], kk[c])));
+            if (AES_T4)
+                s[j][c] = xor3_u32(xor3_u32(q[0], q[1], q[2]), q[3], kk[c]);
+            else
+                s[j][c] = xor3_u32(q[0], q[2], rot8(xor3_u32(q[1], q[3], kk[c])));
         }
 }
 

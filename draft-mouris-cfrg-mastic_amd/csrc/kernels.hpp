@@ -501,6 +501,8 @@ struct AesArgs {
     int np_f;                       // its fill position
     int aes_waves;                  // waves [0, aes_waves) walk parents, the rest are proof waves
     int proof_prio;                 // s_setprio of the proof waves
+    int aes_prio;                   // s_setprio of the AES waves
+    int dbg_skip;                   // timing experiments only (results wrong): 1 = no proof work, 2 = no AES work
 };
 
 // One workgroup = 64 reports (one per lane) x 16 waves: 12 AES waves, each
@@ -557,7 +559,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     const int aes_waves = a.aes_waves;
     if (wave >= aes_waves) {
         // proof wave: node proofs of level - 1 (children seeds from cs_in)
-        if (a.pv_nodes == 0) return;
+        if (a.pv_nodes == 0 || (a.dbg_skip & 1)) return;
         if (a.proof_prio == 1) __builtin_amdgcn_s_setprio(1);
         if (a.proof_prio == 2) __builtin_amdgcn_s_setprio(2);
         const int nbeg = (blockIdx.y * (EVAL_WAVES - aes_waves) + (wave - aes_waves)) * a.pv_npw;
@@ -579,6 +581,9 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         }
         return;
     }
+    if (a.dbg_skip & 2) return;
+    if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (a.aes_prio == 2) __builtin_amdgcn_s_setprio(2);
     const int pbeg = (blockIdx.y * aes_waves + wave) * a.ppw;
     if (pbeg >= a.n_parents) return;
     const int pend = min(pbeg + a.ppw, a.n_parents);

@@ -93,8 +93,11 @@ struct mastic_ctx {
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
+    int n_cus = 256;                     // compute units of the device
     int proof_waves = EVAL_PROOF_WAVES;  // proof waves per eval workgroup (MASTIC_PROOF_WAVES)
     int proof_prio = 0;                  // their s_setprio (MASTIC_PROOF_PRIO)
+    int aes_prio = 0;                    // s_setprio of the AES waves (MASTIC_AES_PRIO)
+    int dbg_skip = 0;                    // timing experiments only (MASTIC_DBG_SKIP; results wrong)
     int stride_pad = 64;                 // words of padding per plane row (MASTIC_STRIDE_PAD)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
@@ -481,6 +484,29 @@ static int choose_ppw(int n_parents, int groups) {
     return (int)std::max(1LL, std::min(per, 64LL));
 }
 
+// Parents per AES wave of the level kernel.  A level is one launch and the
+// next level's launch waits for its last workgroup, so the workgroup count
+// should fill whole rounds of the CUs (one workgroup per CU) with nearly full
+// workgroups: pick, among 8..64 parents per wave, the count whose
+// (work / (rounds x CUs)) is highest, preferring more parents per wave (fewer
+// table fills) within 0.5 %.
+static int choose_eval_ppw(int n_parents, int groups, int aes_waves, int n_cus) {
+    if ((long long)n_parents * groups < (long long)aes_waves * 8 * n_cus) return choose_ppw(n_parents, groups * 2);
+    double best_eff = -1.0;
+    int best = 64;
+    for (int ppw = 64; ppw >= 8; ppw--) {
+        const long long gy = (n_parents + (long long)aes_waves * ppw - 1) / ((long long)aes_waves * ppw);
+        const long long rounds = (groups * gy + n_cus - 1) / n_cus;
+        const double work = (double)groups * n_parents / ((double)aes_waves * ppw);
+        const double eff = work / ((double)rounds * n_cus);
+        if (eff > best_eff + 0.005) {
+            best_eff = eff;
+            best = ppw;
+        }
+    }
+    return best;
+}
+
 static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst_off, const uint32_t* src,
                        size_t src_stride, size_t n, size_t planes) {
     if (planes == 0) return 0;
@@ -558,7 +584,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.level = l;
         a.agg_id = agg_id;
         a.n_parents = np_;
-        a.ppw = choose_ppw(np_, groups * 2);
+        a.ppw = choose_eval_ppw(np_, groups, EVAL_WAVES - c->proof_waves, c->n_cus);
         a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
@@ -571,6 +597,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.force_slow_blk = c->force_slow_blk;
         a.aes_waves = EVAL_WAVES - c->proof_waves;
         a.proof_prio = c->proof_prio;
+        a.aes_prio = c->aes_prio;
+        a.dbg_skip = c->dbg_skip;
         const int gy = (np_ + a.aes_waves * a.ppw - 1) / (a.aes_waves * a.ppw);
         a.pv_level = l - 1;
         a.pv_nodes = l > 0 ? 2 * t->n_parents[l - 1] : 0;
@@ -1151,6 +1179,7 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->user = *up;
     c->p = p;
     c->device = up->device;
+    c->n_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     {
         const char* e = getenv("MASTIC_ABSORB_SINGLE");
         c->absorb_pair = !(e && e[0] == '1');
@@ -1162,6 +1191,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (spd) c->stride_pad = std::max(0, std::min(1 << 20, atoi(spd))) / 64 * 64;
         const char* ap = getenv("MASTIC_ABSORB_PRIO");
         if (ap) c->absorb_prio = std::max(0, std::min(3, atoi(ap)));
+        const char* dsk = getenv("MASTIC_DBG_SKIP");
+        if (dsk) c->dbg_skip = atoi(dsk);
+        const char* xp = getenv("MASTIC_AES_PRIO");
+        if (xp) c->aes_prio = std::max(0, std::min(2, atoi(xp)));
         const char* pp = getenv("MASTIC_PROOF_PRIO");
         if (pp) c->proof_prio = std::max(0, std::min(2, atoi(pp)));
         const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
