@@ -505,17 +505,17 @@ struct AesArgs {
     int dbg_skip;                   // timing experiments only (results wrong): 1 = no proof work, 2 = no AES work
 };
 
-// One workgroup = 64 reports (one per lane) x 16 waves: 12 AES waves, each
-// walking its own run of this level's parents, and 4 proof waves computing
-// the node proofs of the previous level's children (a Keccak-p per node,
-// VALU only).  Specialised waves put LDS-bound AES and VALU-bound Keccak on
-// every CU at a fixed ratio, in one launch, instead of two kernels competing
-// for CU slots.  LDS: the v_perm-addressed T0/T2 table (64 KiB,
+// One workgroup = 64 reports (one per lane) x 16 waves: 8 AES waves walk
+// this level's parents and 8 proof waves first compute the node proofs of the
+// previous level's children (a Keccak-p per node, VALU only), then join the
+// AES waves; parents are claimed in runs through an LDS counter.  LDS-bound
+// AES and VALU-bound Keccak share every CU inside one launch instead of two
+// kernels competing for CU slots.  LDS: the v_perm-addressed T0/T2 table (64 KiB,
 // aes.hpp AesPerm) and the 64 reports' two AES key schedules (22 KiB, one
 // ds_read_b128 per round) are shared by all 16 waves: 86 KiB per workgroup,
 // one workgroup = 4 waves per SIMD per CU.
 #define EVAL_WAVES 16
-#define EVAL_PROOF_WAVES 4  // default split (mastic_ctx::proof_waves)
+#define EVAL_PROOF_WAVES 8  // default split (mastic_ctx::proof_waves); measured best of 2..12
 // VGPR cap of the level kernel: 4 waves x 96 per SIMD leave 128 of the 512
 // for one binder-sponge wave (k_absorb_pair), so the two kernels can share a
 // CU instead of taking turns.
@@ -524,7 +524,7 @@ struct AesArgs {
 #define EVAL_MIN_WAVES 5
 #endif
 #define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(EVAL_MIN_WAVES)))
-#define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16)
+#define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16 + 16)
 // QUAD: payload refills of 2 blocks per sibling (4-block lockstep AES) instead
 // of 1 (paired); chosen at run time (mastic_ctx::eval_quad).
 template <class F, bool QUAD>
@@ -537,6 +537,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     uint32_t* T = (uint32_t*)eval_lds;
     uint4* RKE = eval_lds + AES_PERM_LDS_WORDS / 4;
     uint4* RKC = RKE + 64 * 11;
+    uint32_t* next_parent = (uint32_t*)(RKC + 64 * 11);  // the workgroup's parent-run counter
     // the T-table lookups use the v_perm result as the absolute LDS address
     // (aes.hpp lds_read_asm): the table must start at LDS address 0
     if ((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)eval_lds != 0u) __builtin_trap();
@@ -555,6 +556,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             kc[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_conv + (size_t)i * S, lb));
         }
     }
+    if (threadIdx.x == 0) *next_parent = 0u;
     __syncthreads();
     const int aes_waves = a.aes_waves;
     if (wave >= aes_waves) {
@@ -579,14 +581,26 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             node_proof_one(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
                            [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * 64, lt, w); });
         }
-        return;
+        if (a.proof_prio) __builtin_amdgcn_s_setprio(0);
+        // then help with this workgroup's parents (below)
     }
     if (a.dbg_skip & 2) return;
     if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
     if (a.aes_prio == 2) __builtin_amdgcn_s_setprio(2);
-    const int pbeg = (blockIdx.y * aes_waves + wave) * a.ppw;
-    if (pbeg >= a.n_parents) return;
-    const int pend = min(pbeg + a.ppw, a.n_parents);
+    // Parents of this workgroup: [wp0, wp1), claimed in runs of `run` by
+    // every wave through an LDS counter: the proof waves join once their
+    // proofs are done, so no wave idles while another still has parents.
+    const int wp0 = blockIdx.y * aes_waves * a.ppw;
+    const int wp1 = min(wp0 + aes_waves * a.ppw, a.n_parents);
+    const int run = max(1, a.ppw / 8);
+    auto claim = [&]() -> int {
+        uint32_t o = 0;
+        if (lane == 0) o = atomicAdd(next_parent, (uint32_t)run);
+        return wp0 + (int)__builtin_amdgcn_readfirstlane(o);
+    };
+    int rbeg = claim();
+    if (rbeg >= wp1) return;
+    int rend = min(rbeg + run, wp1);
     const int l = a.level;
     const int vl = p.value_len;
     const int wl = vl * F::W32;
@@ -616,15 +630,22 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         }
     };
     uint32_t nps[4], npctrl;
-    load_parent(pbeg, nps, npctrl);
-    for (int pi = pbeg; pi < pend; pi++) {
+    load_parent(rbeg, nps, npctrl);
+    for (int pi = rbeg; pi >= 0;) {
         // The key schedules are re-read from LDS (one ds_read_b128 per round):
         // without the barrier the compiler hoists all 22 reads out of the loop
         // and pins 88 VGPRs.
         asm volatile("" ::: "memory");
         uint32_t ps[4] = {nps[0], nps[1], nps[2], nps[3]};
         const uint32_t pctrl = npctrl;
-        if (pi + 1 < pend) load_parent(pi + 1, nps, npctrl);
+        // next parent: the rest of this run, else a new run
+        int nxt = pi + 1;
+        if (nxt == rend) {
+            rbeg = claim();
+            rend = min(rbeg + run, wp1);
+            nxt = rbeg < wp1 ? rbeg : -1;
+        }
+        if (nxt >= 0) load_parent(nxt, nps, npctrl);
         // extend: block 0 -> left child, block 1 -> right child (one paired
         // AES call), correct, then both children's convert seed blocks.
         uint32_t cs0[4], cs1[4], ns0[4], ns1[4];
@@ -744,6 +765,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 }
             }
         }
+        pi = nxt;
     }
 }
 

@@ -1186,7 +1186,7 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         const char* l = getenv("MASTIC_ABSORB_LDS_KB");
         c->absorb_lds = l ? std::max(0, std::min(160, atoi(l))) * 1024 : 0;
         const char* pw = getenv("MASTIC_PROOF_WAVES");
-        if (pw) c->proof_waves = std::max(1, std::min(8, atoi(pw)));
+        if (pw) c->proof_waves = std::max(1, std::min(15, atoi(pw)));
         const char* spd = getenv("MASTIC_STRIDE_PAD");
         if (spd) c->stride_pad = std::max(0, std::min(1 << 20, atoi(spd))) / 64 * 64;
         const char* ap = getenv("MASTIC_ABSORB_PRIO");
