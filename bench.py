@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reports", type=int, default=8192, help="reports per rank per step")
+    ap.add_argument("--reports", type=int, default=12288, help="reports per rank per step")
     ap.add_argument("--prefixes", type=int, default=10000)
     ap.add_argument("--agg-id", type=int, default=0)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU baseline leg")

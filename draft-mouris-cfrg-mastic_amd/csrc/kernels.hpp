@@ -496,6 +496,7 @@ struct AesArgs {
     const uint32_t* pv_child_path;  // [pv_nodes][8]
     uint32_t* pv_onehot;            // [pv_nodes * 8] proofs of level - 1 (tiled, see AbsorbArgs)
     int oh_gstride;                 // words per report group of the proof buffers
+    int bin_rstride;                // words between consecutive words of a report in them
     int pay_gstride;                // ... of the payload-difference buffers
     const PrefixState* np;          // node-proof prefix state
     int np_f;                       // its fill position
@@ -579,7 +580,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_in + ((size_t)node * 5 + i) * S, lb);
             const uint32_t t = pld(a.cs_in + ((size_t)node * 5 + 4) * S, lb);
             node_proof_one(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
-                           [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * 64, lt, w); });
+                           [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
         }
         if (a.proof_prio) __builtin_amdgcn_s_setprio(0);
         // then help with this workgroup's parents (below)
@@ -690,7 +691,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 const E d = F::sub(F::sub(wp, x0), x1);
 #pragma unroll
                 for (int i = 0; i < F::W32; i++)
-                    pst(payg + ((size_t)(pi * vl + e) * F::W32 + i) * 64, (uint32_t)lane * 4u, F::word(d, i));
+                    pst(payg + ((size_t)(pi * vl + e) * F::W32 + i) * a.bin_rstride, (uint32_t)lane * 4u,
+                        F::word(d, i));
             }
             if (pf0 >= 0 || pf1 >= 0) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
@@ -778,6 +780,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 // line XOR pattern, so no LDS staging and no per-lane indexing is needed.
 struct ProofArgs {
     int oh_gstride;      // words per report group of the (tiled) proof buffer
+    int bin_rstride;     // words between consecutive words of a report
     int level;
     int n_nodes;
     int npw;             // nodes per wave
@@ -810,7 +813,7 @@ __global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, Proof
         for (int i = 0; i < 4; i++) seed[i] = pld(a.cs + ((size_t)node * 5 + i) * S, lb);
         const uint32_t t = pld(a.cs + ((size_t)node * 5 + 4) * S, lb);
         node_proof_one(a.np, a.f, p.bits, l, a.path_bytes, seed, a.child_path + node * 8, t, pcw,
-                       [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * 64, lt, w); });
+                       [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
     }
 }
 
@@ -824,7 +827,8 @@ __global__ __launch_bounds__(256) void k_node_proof(McParams p, Planes pl, Proof
 // 256-byte row.
 struct AbsorbArgs {
     const uint32_t* seg[2];
-    int gstride[2];  // words per report group of each tiled segment
+    int gstride[2];  // words per report group of each segment (planes: 64)
+    int rstride;     // words between consecutive stream words of a report (tiled: 64, planes: stride)
     int nbytes[2];
     int f[2];
     int prio;  // s_setprio of the sponge waves (0..3)
@@ -857,6 +861,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     const uint32_t* seg = a.seg[which] + (size_t)(r >> 6) * a.gstride[which];  // this wave's tile group
     const uint32_t lb = (uint32_t)r * 4u;
     const uint32_t lt = (uint32_t)(r & 63) * 4u;  // lane offset inside a tile row
+    const uint32_t rowb = (uint32_t)a.rstride * 4u;  // bytes between stream words
     KState s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = u32x2{pld(sp + (size_t)(2 * i) * S, lb), pld(sp + (size_t)(2 * i + 1) * S, lb)};
@@ -870,7 +875,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     auto load_block = [&](int b, uint32_t* w) {
         const int base = KECCAK_RATE_WORDS * b - q - off;
         if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
-            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * 64);
+            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * a.rstride);
             // the row offset is a running SGPR sum made opaque at every step,
             // so the compiler cannot hoist 43 loop-invariant offsets (which it
             // would spill to VGPRs and then waterfall)
@@ -878,7 +883,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
                 w[j] = pld_so(rs, lt, so);
-                so += 256u;
+                so += rowb;
                 asm volatile("" : "+s"(so));
             }
         } else {
@@ -886,7 +891,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
                 const int m = base + j;
                 const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-                w[j] = pld(seg + (size_t)mc * 64, lt);
+                w[j] = pld(seg + (size_t)mc * a.rstride, lt);
             }
 #pragma unroll
             for (int j = 0; j < KECCAK_RATE_WORDS + 1; j++) {
@@ -925,7 +930,7 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     // (launched with optional dynamic LDS that is never touched: it only caps
     // how many absorb workgroups share a CU, see mastic_ctx::absorb_lds)
     const int h = threadIdx.x & 1;
-    const int r = blockIdx.x * 128 + (threadIdx.x >> 1);
+    const int r = blockIdx.x * (int)(blockDim.x >> 1) + (int)(threadIdx.x >> 1);
     const int which = blockIdx.y;
     if (r >= pl.stride) return;  // both lanes of a pair leave together
     const int nb = a.nbytes[which];
@@ -935,7 +940,8 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     const uint32_t* seg = a.seg[which] + (size_t)(r >> 6) * a.gstride[which];  // this wave's tile group
     const uint32_t lbh = ((uint32_t)h * (uint32_t)S + (uint32_t)r) * 4u;  // state plane h of the pair
     const uint32_t lt = (uint32_t)(r & 63) * 4u;                            // lane offset in a tile row
-    const uint32_t lth = lt + (uint32_t)h * 256u;                           // ... of the next row for h = 1
+    const uint32_t rowb = (uint32_t)a.rstride * 4u;                          // bytes between stream words
+    const uint32_t lth = lt + (uint32_t)h * rowb;                           // ... of the next word for h = 1
     KHalf s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = pld(sp + (size_t)(2 * i) * S, lbh);
@@ -950,12 +956,12 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     auto load_block = [&](int b, uint32_t* w) {
         const int base = KECCAK_RATE_WORDS * b - q - off;
         if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
-            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * 64);
+            const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * a.rstride);
             uint32_t so = 0;  // running opaque row offset, as in k_absorb
 #pragma unroll
             for (int k = 0; k < NL; k++) {
                 w[k] = pld_so(rs, lth, so);
-                so += 256u;
+                so += rowb;
                 asm volatile("" : "+s"(so));
             }
         } else {
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
             for (int k = 0; k < NL + 1; k++) {
                 const int m = base + k;
                 const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-                t[k] = pld(seg + (size_t)mc * 64, lt);
+                t[k] = pld(seg + (size_t)mc * a.rstride, lt);
             }
 #pragma unroll
             for (int k = 0; k < NL + 1; k++) {

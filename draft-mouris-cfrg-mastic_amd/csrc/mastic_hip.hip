@@ -99,6 +99,8 @@ struct mastic_ctx {
     int aes_prio = 0;                    // s_setprio of the AES waves (MASTIC_AES_PRIO)
     int dbg_skip = 0;                    // timing experiments only (MASTIC_DBG_SKIP; results wrong)
     int stride_pad = 64;                 // words of padding per plane row (MASTIC_STRIDE_PAD)
+    bool binder_tiled = true;            // tiled level binder buffers (MASTIC_BINDER_TILED=0: planes)
+    int absorb_threads = 256;            // threads per binder-sponge workgroup (MASTIC_ABSORB_THREADS)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
@@ -547,8 +549,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     size_t sev = 0;
     std::vector<hipEvent_t> abs_done(t->L + 1);
     // tiled level buffers (kernels.hpp AbsorbArgs): words per report group
-    const int oh_gstride = t->max_level_nodes * 8 * 64;
-    const int pay_gstride = t->max_parents * wlw * 64;
+    // (MASTIC_BINDER_TILED=0: plane layout, i.e. group stride 64, row stride = stride)
+    const int oh_gstride = c->binder_tiled ? t->max_level_nodes * 8 * 64 : 64;
+    const int pay_gstride = c->binder_tiled ? t->max_parents * wlw * 64 : 64;
+    const int bin_rstride = c->binder_tiled ? 64 : stride;
     auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
         const int slot = lv % NSLOT;
         AbsorbArgs ab;
@@ -558,14 +562,15 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         ab.f[0] = f_oh;
         ab.seg[1] = plane(wl.payload[slot]);
         ab.gstride[1] = pay_gstride;
+        ab.rstride = bin_rstride;
         ab.nbytes[1] = lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
         ab.f[1] = f_pl;
         ab.prio = c->absorb_prio;
         HIPCHK(c, hipStreamWaitEvent(c->stream2, ready, 0));
         HIPCHK(c, hipEventRecord(e4, c->stream2));
         if (c->absorb_pair)
-            hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 + 127) / 128, 2), dim3(256), c->absorb_lds,
-                               c->stream2, pl, ab);
+            hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, 2),
+                               dim3(c->absorb_threads), c->absorb_lds, c->stream2, pl, ab);
         else
             hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
         HIPCHK(c, hipEventRecord(e5, c->stream2));
@@ -608,6 +613,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.pv_onehot = l > 0 ? plane(wl.onehot[(l - 1) % NSLOT]) : nullptr;
         a.oh_gstride = oh_gstride;
         a.pay_gstride = pay_gstride;
+        a.bin_rstride = bin_rstride;
         a.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         a.np_f = c->pfx_f[PFX_NODE];
         dim3 grid(groups, gy);
@@ -642,6 +648,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         pa.cs = plane(wl.cs[l & 1]);
         pa.onehot = plane(wl.onehot[l % NSLOT]);
         pa.oh_gstride = oh_gstride;
+        pa.bin_rstride = bin_rstride;
         pa.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         pa.f = c->pfx_f[PFX_NODE];
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
@@ -1189,6 +1196,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (pw) c->proof_waves = std::max(1, std::min(15, atoi(pw)));
         const char* spd = getenv("MASTIC_STRIDE_PAD");
         if (spd) c->stride_pad = std::max(0, std::min(1 << 20, atoi(spd))) / 64 * 64;
+        const char* bt = getenv("MASTIC_BINDER_TILED");
+        if (bt) c->binder_tiled = bt[0] != '0';
+        const char* at = getenv("MASTIC_ABSORB_THREADS");
+        if (at) c->absorb_threads = std::max(64, std::min(256, atoi(at))) / 64 * 64;
         const char* ap = getenv("MASTIC_ABSORB_PRIO");
         if (ap) c->absorb_prio = std::max(0, std::min(3, atoi(ap)));
         const char* dsk = getenv("MASTIC_DBG_SKIP");
