@@ -1,5 +1,5 @@
 """Benchmark: VIDPF report x prefix evaluations/sec for Mastic prep_init +
-aggregate on MI355X (BASELINE.json metric), config C2:
+aggregate on MI355X (BASELINE.json metric).  Default config C2 (the metric's headline):
 Mastic(BITS=32, Sum max=255), 10k candidate prefixes at level 31, weight
 check on, leader side (agg_id 0).
 
@@ -9,7 +9,7 @@ aggregate fold of all out shares; with N > 1 ranks also the RCCL all-gather
 of the per-rank agg shares and the on-GPU mod-p merge.  Reports are sharded
 over ranks (independent units, weak scaling).
 
-    python bench.py [--gpus N --steps K --warmup W --reports R --prefixes P]
+    python bench.py [--gpus N --steps K --warmup W --config c2|c3|c4|c5 --reports R --prefixes P]
     (N > 1: launched by torch.distributed.run, one rank per GPU)
 """
 import argparse
@@ -27,10 +27,28 @@ METRIC = "VIDPF report x prefix evals/sec at 1/2/4/8 GPUs; % of int-VALU peak"
 # Fixed op-cost convention: int32 ops
 AES_BLOCK_OPS = 340
 KECCAK_OPS = 3720
-F64_ADD_OPS = 4
+FIELD_ADD_OPS = 4
 # int32 VALU peak: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
+
+
+# BASELINE.json configs measured on one GPU (C1 is the reference's CPU-sized
+# sweep; it is a parity case, tests/test_gpu_configs.py).  Each entry: Mastic
+# constructor, level, candidate prefixes, default reports per rank per step.
+CONFIGS = {
+    "c2": dict(circuit="Sum", kw=dict(bits=32, max_measurement=255), prefixes=10000, reports=12288,
+               desc="C2: Mastic(BITS=32, Sum max=255) prep_init+aggregate, level 31"),
+    "c3": dict(circuit="Count", kw=dict(bits=256), prefixes=128, reports=16384,
+               desc="C3: Mastic(BITS=256, Count) prep_init+aggregate at level 255 of the threshold-pruned "
+                    "sweep (128 surviving candidates, the Zipf(1.1)/0.05% frontier)"),
+    "c4": dict(circuit="Histogram", kw=dict(bits=64, length=64, chunk_length=8), prefixes=1000, reports=12288,
+               desc="C4: Mastic(BITS=64, Histogram length=64 chunk 8, Field128) prep_init+aggregate, level 63"),
+    "c5": dict(circuit="SumVec", kw=dict(bits=32, length=1024, sum_vec_bits=1, chunk_length=32), prefixes=100,
+               reports=8192,
+               desc="C5: Mastic(BITS=32, SumVec length=1024 bits=1 chunk 32, Field128) prep_init+aggregate, "
+                    "level 31"),
+}
 
 
 def parse():
@@ -38,49 +56,82 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reports", type=int, default=12288, help="reports per rank per step")
-    ap.add_argument("--prefixes", type=int, default=10000)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="BASELINE config (c2 = the metric's headline config)")
+    ap.add_argument("--reports", type=int, default=0, help="reports per rank per step (0 = config default)")
+    ap.add_argument("--prefixes", type=int, default=0, help="candidate prefixes (0 = config default)")
     ap.add_argument("--agg-id", type=int, default=0)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU baseline leg")
     ap.add_argument("--cpu-procs", type=int, default=16)
     return ap.parse_args()
 
 
-def synth(rank, n_reports, n_prefixes, seed=0x4D41 + 2):
-    """Synthetic C2 inputs: 10k random 32-bit attributes,
-    alphas uniform over them, weights uniform 0..255, distinct random nonces."""
+def _attrs(rng, bits, n_prefixes):
+    """n distinct random bits-bit attributes, sorted, as MSB-first byte rows."""
+    if bits == 32:  # the C2 stream of earlier rounds (uint32 draws)
+        attrs = np.unique(rng.integers(0, 2 ** 32, size=n_prefixes, dtype=np.uint64).astype(np.uint32))
+        while len(attrs) < n_prefixes:
+            attrs = np.unique(np.concatenate([attrs, rng.integers(0, 2 ** 32, size=n_prefixes - len(attrs),
+                                                                  dtype=np.uint64).astype(np.uint32)]))
+        return np.sort(attrs).astype(">u4").view(np.uint8).reshape(-1, 4)
+    ab = (bits + 7) // 8
+    rows = np.unique(rng.integers(0, 256, size=(n_prefixes, ab), dtype=np.uint8), axis=0)
+    return rows  # np.unique sorts rows lexicographically (= MSB-first path order)
+
+
+def synth(m, cfg, rank, n_reports, n_prefixes, seed):
+    """Synthetic inputs: random attributes, alphas uniform over
+    them, weights per the circuit, distinct random nonces per report."""
     rng = np.random.default_rng(seed)
-    attrs = np.unique(rng.integers(0, 2 ** 32, size=n_prefixes, dtype=np.uint64).astype(np.uint32))
-    while len(attrs) < n_prefixes:
-        attrs = np.unique(np.concatenate([attrs, rng.integers(0, 2 ** 32, size=n_prefixes - len(attrs),
-                                                              dtype=np.uint64).astype(np.uint32)]))
-    attrs = np.sort(attrs)
+    attrs = _attrs(rng, cfg["kw"]["bits"], n_prefixes)
     rrng = np.random.default_rng(seed * 1000003 + rank)
     alphas = attrs[rrng.integers(0, len(attrs), size=n_reports)]
-    weights = rrng.integers(0, 256, size=n_reports)
+    betas = encode_betas(m, cfg, n_reports, rrng)
     nonces = rrng.integers(0, 256, size=16 * n_reports, dtype=np.uint8).tobytes()
-    return attrs, alphas, weights, nonces, rrng
+    rands = rrng.integers(0, 256, size=m.RAND_SIZE * n_reports, dtype=np.uint8).tobytes()
+    return attrs, alphas.tobytes(), betas, nonces, rands
 
 
-def encode_inputs(m, alphas, weights, rrng):
-    n = len(alphas)
-    alpha_b = alphas.astype(">u4").tobytes()  # MSB-first 32-bit paths
-    bits = ((weights[:, None] >> np.arange(8)) & 1).astype("<u8")  # Sum(255): b = 8, offset 0
-    betas = np.concatenate([bits, bits], axis=1).tobytes()
-    rands = rrng.integers(0, 256, size=m.RAND_SIZE * n, dtype=np.uint8).tobytes()
-    return alpha_b, betas, rands
+def encode_betas(m, cfg, n, rrng):
+    """Valid.encode of random measurements, encode_vec'd (ENC bytes LE per element)."""
+    c = cfg["circuit"]
+    dt = "<u8"
+    if c == "Sum":  # Sum(255): b = 8, offset 0 -> bits(w) || bits(w)
+        w = rrng.integers(0, 256, size=n)
+        bits = ((w[:, None] >> np.arange(8)) & 1).astype(dt)
+        return np.concatenate([bits, bits], axis=1).tobytes()
+    if c == "Count":
+        return (rrng.random(n) < 0.9).astype(dt).tobytes()
+    if c == "Histogram":
+        e = np.zeros((n, m.length, 2), dtype=dt)
+        e[np.arange(n), rrng.integers(0, m.length, size=n), 0] = 1
+        return e.tobytes()
+    # SumVec bits=1: one field element per bit
+    e = np.zeros((n, m.length, 2), dtype=dt)
+    e[:, :, 0] = rrng.integers(0, 2, size=(n, m.length))
+    return e.tobytes()
 
 
-def agg_param_bytes(attrs):
-    return (31).to_bytes(2, "big") + len(attrs).to_bytes(4, "big") + attrs.astype(">u4").tobytes() + b"\x01"
+def agg_param_bytes(level, attrs):
+    return level.to_bytes(2, "big") + len(attrs).to_bytes(4, "big") + attrs.tobytes() + b"\x01"
 
 
 # ---------------------------------------------------------------- CPU baseline
 def _cpu_worker(job):
-    (enc_ap, nonce, pub, ins, vk, ctx, agg_id) = job
+    (spec, enc_ap, nonce, pub, ins, vk, ctx, agg_id) = job
     sys.path.insert(0, ROOT)
-    from oracle.mastic import MasticSum
-    o = MasticSum(32, 255)
+    from oracle import mastic as om
+    (circuit, kw) = spec
+    kw = dict(kw)
+    bits = kw.pop("bits")
+    if circuit == "Sum":
+        o = om.MasticSum(bits, kw["max_measurement"])
+    elif circuit == "Count":
+        o = om.MasticCount(bits)
+    elif circuit == "Histogram":
+        o = om.MasticHistogram(bits, kw["length"], kw["chunk_length"])
+    else:
+        o = om.MasticSumVec(bits, kw["length"], kw["sum_vec_bits"], kw["chunk_length"])
     ap = o.decode_agg_param(enc_ap)
     cws = o.vidpf.decode_public_share(pub)
     isd = o.decode_input_share(agg_id, ins)
@@ -114,15 +165,20 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from mastic_amd import MasticSum
+    from mastic_amd import Mastic
     from mastic_amd.merge import merge_agg_shares
 
-    m = MasticSum(32, 255, device=local)
+    cfg = CONFIGS[args.config]
+    n_rep = args.reports or cfg["reports"]
+    n_pre = args.prefixes or cfg["prefixes"]
+    kw = dict(cfg["kw"])
+    bits = kw.pop("bits")
+    m = Mastic(bits, cfg["circuit"], device=local, **kw)
     ctx = b"mastic-mi355x-bench"
-    attrs, alphas, weights, nonces, rrng = synth(rank, args.reports, args.prefixes)
-    alpha_b, betas, rands = encode_inputs(m, alphas, weights, rrng)
+    seed = 0x4D41 + int(args.config[1])
+    attrs, alpha_b, betas, nonces, rands = synth(m, cfg, rank, n_rep, n_pre, seed)
     vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
-    enc_ap = agg_param_bytes(attrs)
+    enc_ap = agg_param_bytes(bits - 1, attrs)
     reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
     (nodes, interior, _maxl) = m.tree_stats(enc_ap)
 
@@ -160,16 +216,17 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    units = args.reports * len(attrs) * args.steps * world
+    units = n_rep * len(attrs) * args.steps * world
     value = units / dt
     # roofline of the dominant kernel: algorithmic int32 ops (fixed convention).
     # k_eval_aes runs each level's AES (extend, convert: 1 + ceil(VL*ENC/16) blocks, payload
     # adds) and, in its proof waves, the previous level's node proofs (one Keccak-p per node);
     # the last level's proofs run in k_node_proof, so the pair is timed together.
     aes_per_node = 1 + (16 + m.VALUE_LEN * m.field.ENCODED_SIZE + 15) // 16
-    aes_ops_node = aes_per_node * AES_BLOCK_OPS + 2 * m.VALUE_LEN * F64_ADD_OPS
-    node_units = nodes * args.reports * args.steps
-    dom = "k_eval_aes<F64> (+ node-proof waves, + k_node_proof for the last level)"
+    aes_ops_node = aes_per_node * AES_BLOCK_OPS + 2 * m.VALUE_LEN * FIELD_ADD_OPS
+    node_units = nodes * n_rep * args.steps
+    fname = "F64" if m.field.ENCODED_SIZE == 8 else "F128"
+    dom = "k_eval_aes<%s> (+ node-proof waves, + k_node_proof for the last level)" % fname
     dom_ms = aes_ms + proof_ms
     dom_ops = aes_ops_node + KECCAK_OPS
     achieved = node_units * dom_ops / (dom_ms / 1e3) / 1e12 if dom_ms > 0 else 0.0
@@ -189,12 +246,13 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {
-            "workload": "C2: Mastic(BITS=32, Sum max=255) prep_init+aggregate, %d reports x %d prefixes per "
-                        "rank per step, level 31, weight check, agg_id %d" % (args.reports, len(attrs), args.agg_id),
-            "reports_per_step": args.reports * world,
+            "workload": "%s, %d reports x %d prefixes per rank per step, weight check, agg_id %d"
+                        % (cfg["desc"], n_rep, len(attrs), args.agg_id),
+            "reports_per_step": n_rep * world,
             "prefixes": len(attrs),
             "nodes_per_report": nodes,
-            "field": "Field64",
+            "work_bytes_per_report": m.work_bytes(enc_ap),
+            "field": "Field64" if fname == "F64" else "Field128",
             "parallelism": "reports sharded %d-way" % world,
         },
         "roofline": {
@@ -214,7 +272,7 @@ def main():
             "node_proof_last_level": proof_ms / args.steps,
             "absorb": absorb_ms / args.steps,
             "prep_init_total": total_ms / args.steps,
-            "frac_int_valu_whole_step": (node_units * (aes_ops_node + KECCAK_OPS) + absorb_perms * args.reports *
+            "frac_int_valu_whole_step": (node_units * (aes_ops_node + KECCAK_OPS) + absorb_perms * n_rep *
                                          args.steps * KECCAK_OPS) / (dt * 1e12) / VALU_PEAK_TOPS,
             "absorb_keccak_perms_per_report": absorb_perms,
         },
@@ -222,7 +280,8 @@ def main():
     traffic_file = os.path.join(ROOT, "profiles", "eval_traffic.json")
     if os.path.exists(traffic_file):
         tr = json.load(open(traffic_file))
-        if tr.get("prefixes") == len(attrs) and tr.get("reports") == args.reports:
+        if (tr.get("config", "c2") == args.config and tr.get("prefixes") == len(attrs)
+                and tr.get("reports") == n_rep):
             out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
 
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -231,7 +290,8 @@ def main():
         ps = m.sizes.public_share_size
         isz = m.sizes.input_share_size[args.agg_id]
         ins = in0 if args.agg_id == 0 else in1
-        jobs = [(enc_ap, rn[16 * i:16 * (i + 1)], pub[ps * i:ps * (i + 1)], ins[isz * i:isz * (i + 1)], vk, ctx,
+        spec = (cfg["circuit"], cfg["kw"])
+        jobs = [(spec, enc_ap, rn[16 * i:16 * (i + 1)], pub[ps * i:ps * (i + 1)], ins[isz * i:isz * (i + 1)], vk, ctx,
                  args.agg_id) for i in range(procs)]
         wall, res = cpu_baseline(jobs, procs)
         # the same reports through the GPU path: parity of the timed workload

@@ -721,29 +721,41 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
         auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + e, S, r) : F::zero(); };
         int e_fast = 0;  // elements completed by the fast path
-        if constexpr (F::W32 == 2 && !QUAD) {
-            // Field64 fast path: block b (counter b + 1) of each child's convert
-            // stream holds candidates 2b and 2b + 1 (vdaf_poc next_vec after
-            // next(16)).  Speculate that no candidate is rejected: one paired AES
-            // call per block index, straight-line.  A candidate >= p has its high
-            // word 0xffffffff (probability 2^-32); if any lane of the wave sees
+        if constexpr (!QUAD) {
+            // Fast path: block b (counter b + 1) of each child's convert stream
+            // holds Field64 candidates 2b and 2b + 1, or Field128 candidate b
+            // (vdaf_poc next_vec after next(16)).  Speculate that no candidate
+            // is rejected: one paired AES call per block index, straight-line.
+            // A candidate >= p has its top word 0xffffffff (probability 2^-32
+            // for Field64, ~2^-59 for Field128); if any lane of the wave sees
             // such a word among the elements it is about to use, the exact
             // stream below redoes this parent from that element on (elements
             // before it are unaffected by the rejection).
-            const int nblk = (vl + 1) >> 1;
+            constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
+            const int nblk = (vl + EPB - 1) / EPB;
             for (int b = 0; b < nblk; b++) {
                 asm volatile("" ::: "memory");
-                const int e = 2 * b;
-                const bool two = e + 1 < vl;
+                const int e = EPB * b;
+                const bool two = EPB == 2 && e + 1 < vl;
                 const int e1 = two ? e + 1 : e;  // uniform clamp
-                const E cwa = load_cw(e), cwb = load_cw(e1);
-                const E wpa = load_wp(e), wpb = load_wp(e1);
+                const E cwa = load_cw(e), wpa = load_wp(e);
+                E cwb = cwa, wpb = wpa;
+                if constexpr (EPB == 2) {
+                    cwb = load_cw(e1);
+                    wpb = load_wp(e1);
+                }
                 uint32_t o0[4], o1[4];
                 fixed_key_block2(TL, rkc, cs0, (uint32_t)(b + 1), cs1, (uint32_t)(b + 1), o0, o1);
-                const bool sus = (o0[1] == ~0u) | (o1[1] == ~0u) | (two & ((o0[3] == ~0u) | (o1[3] == ~0u)));
+                bool sus;
+                if constexpr (EPB == 2)
+                    sus = (o0[1] == ~0u) | (o1[1] == ~0u) | (two & ((o0[3] == ~0u) | (o1[3] == ~0u)));
+                else
+                    sus = (o0[3] == ~0u) | (o1[3] == ~0u);
                 if (__builtin_expect(__any(sus), 0) || b == a.force_slow_blk) break;
                 emit(e, F::from_words(o0), F::from_words(o1), cwa, wpa);
-                if (two) emit(e + 1, F::from_words(o0 + 2), F::from_words(o1 + 2), cwb, wpb);
+                if constexpr (EPB == 2) {
+                    if (two) emit(e + 1, F::from_words(o0 + 2), F::from_words(o1 + 2), cwb, wpb);
+                }
                 e_fast = e + 1 + (two ? 1 : 0);
             }
         }

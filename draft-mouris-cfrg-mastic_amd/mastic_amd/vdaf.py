@@ -299,6 +299,14 @@ class Mastic:
                                                        ctypes.byref(b), ctypes.byref(c)))
         return (a.value, b.value, c.value)
 
+    def work_bytes(self, agg_param):
+        """HBM work bytes per report of one prep_init at this agg param
+        (batches larger than the memory budget allows are run in chunks)."""
+        enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
+        v = ctypes.c_uint64()
+        _check(self._ctx, _lib.lib().mastic_work_bytes(self._ctx, enc, len(enc), ctypes.byref(v)))
+        return v.value
+
     @staticmethod
     def _agg_param_header(enc: bytes):
         if len(enc) < 7:

@@ -365,3 +365,17 @@ def test_fast_path_handover_to_exact_stream(mastic_amd, blk, monkeypatch):
     vk = bytes(rng.getrandbits(8) for _ in range(32))
     ap = _random_agg_param(m, rng, alphas, 5, 5, True)
     _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=False)
+
+
+@pytest.mark.parametrize("blk", [0, 2, 6])
+def test_fast_path_handover_field128(mastic_amd, blk, monkeypatch):
+    """Same handover for the Field128 fast path (one candidate per block; a
+    candidate >= p has its top word 0xffffffff)."""
+    monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
+    rng = random.Random(200 + blk)
+    m = mastic_amd.MasticHistogram(5, 7, 3)  # VALUE_LEN 8: 8 payload blocks per node
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 4)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    ap = _random_agg_param(m, rng, alphas, 4, 5, True)
+    _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=False)
