@@ -233,19 +233,24 @@ struct AesPerm {
     const uint32_t* T;  // the table; must sit at LDS address 0 (see lds_read_asm)
     uint32_t lb0;       // 4 * (lane & 31)
     uint32_t lb2;       // 128 + 4 * (lane & 31)
+    // v_perm_b32 issues at half rate (4 cycles per wave64 instruction on a
+    // SIMD, tools/valu_peak.hip); byte 1 already sits at address bits 8..15,
+    // so its address is a bitwise select (x & 0xff00) | (lane & ~0xff00): ONE
+    // full-rate v_bitop3_b32 (LUT 0xE4 = src2 ? src0 : src1).
     template <int K>
-    MH_D uint32_t a0(uint32_t x) const { return __builtin_amdgcn_perm(x, lb0, 0x0c0c0000u | ((4u + K) << 8)); }
+    MH_D static uint32_t addr(uint32_t x, uint32_t lane, uint32_t sel_hi) {
+        if constexpr (K == 1) return __builtin_amdgcn_bitop3_b32(x, lane, 0xff00u, 0xE4);
+        return __builtin_amdgcn_perm(x, lane, sel_hi | ((4u + K) << 8));
+    }
     template <int K>
-    MH_D uint32_t a2(uint32_t x) const { return __builtin_amdgcn_perm(x, lb2, 0x0c0c0000u | ((4u + K) << 8)); }
+    MH_D uint32_t a0(uint32_t x) const { return addr<K>(x, lb0, 0x0c0c0000u); }
+    template <int K>
+    MH_D uint32_t a2(uint32_t x) const { return addr<K>(x, lb2, 0x0c0c0000u); }
     // T1 / T3 (AES_T4): same lane bytes plus 0x01 in byte 2 -> +64 KiB
     template <int K>
-    MH_D uint32_t a1(uint32_t x) const {
-        return __builtin_amdgcn_perm(x, lb0 | 0x10000u, 0x0c020000u | ((4u + K) << 8));
-    }
+    MH_D uint32_t a1(uint32_t x) const { return addr<K>(x, lb0 | 0x10000u, 0x0c020000u); }
     template <int K>
-    MH_D uint32_t a3(uint32_t x) const {
-        return __builtin_amdgcn_perm(x, lb2 | 0x10000u, 0x0c020000u | ((4u + K) << 8));
-    }
+    MH_D uint32_t a3(uint32_t x) const { return addr<K>(x, lb2 | 0x10000u, 0x0c020000u); }
     template <int K>
     MH_D uint32_t t0(uint32_t x) const { return *(const uint32_t*)((const char*)T + a0<K>(x)); }
     template <int K>
