@@ -277,12 +277,14 @@ def main():
             "absorb_keccak_perms_per_report": absorb_perms,
         },
     }
+    # HBM bytes per launch of the dominant kernel from the PMC passes (profiles/eval_traffic.json),
+    # when they were measured at this exact workload
     traffic_file = os.path.join(ROOT, "profiles", "eval_traffic.json")
     if os.path.exists(traffic_file):
-        tr = json.load(open(traffic_file))
-        if (tr.get("config", "c2") == args.config and tr.get("prefixes") == len(attrs)
-                and tr.get("reports") == n_rep):
-            out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        for tr in json.load(open(traffic_file)).get("entries", []):
+            if tr["config"] == args.config and tr["prefixes"] == len(attrs) and tr["reports"] == n_rep:
+                out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+                out["roofline"]["traffic_unit"] = "bytes per launch"
 
     if rank == 0 and world == 1 and args.cpu_baseline:
         procs = min(args.cpu_procs, os.cpu_count() or 1)

@@ -27,7 +27,7 @@ def load(path):
     return dur, n, vals
 
 
-def main(d, kernels=("k_eval_aes<F64>", "k_node_proof", "k_absorb_pair", "k_absorb")):
+def main(d, kernels=("k_eval_aes<F64>", "k_eval_aes<F128>", "k_node_proof", "k_absorb_pair", "k_absorb")):
     out = {}
     dur, n, sq1 = load(os.path.join(d, "sq1/run_counter_collection.csv"))
     _, _, sq2 = load(os.path.join(d, "sq2/run_counter_collection.csv"))
@@ -43,7 +43,11 @@ def main(d, kernels=("k_eval_aes<F64>", "k_node_proof", "k_absorb_pair", "k_abso
         out[k] = {
             "launches": n[k],
             "serial_ms": ms,
-            "valu_busy": v1["SQ_INSTS_VALU"] * 4 / (cyc * CUS * 4),
+            # wave64 VALU issue: 2 cycles per instruction on a SIMD for full-rate ops
+            # (v_xor/v_bitop3/v_add), 4 for half-rate ones (v_perm/v_alignbit/v_bfe/...):
+            # profiles/r01_v9_valu_peak.json (tools/valu_peak.hip).  The two bounds:
+            "valu_busy_if_all_full_rate": v1["SQ_INSTS_VALU"] * 2 / (cyc * CUS * 4),
+            "valu_busy_if_all_half_rate": v1["SQ_INSTS_VALU"] * 4 / (cyc * CUS * 4),
             "lds_busy": v2["SQ_LDS_IDX_ACTIVE"] / (cyc * CUS),
             "wait_any_over_active": v2["SQ_WAIT_ANY"] / act,
             "wait_inst_any_over_active": v2["SQ_WAIT_INST_ANY"] / act,
