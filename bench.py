@@ -42,6 +42,10 @@ CONFIGS = {
     "c3": dict(circuit="Count", kw=dict(bits=256), prefixes=128, reports=16384,
                desc="C3: Mastic(BITS=256, Count) prep_init+aggregate at level 255 of the threshold-pruned "
                     "sweep (128 surviving candidates, the Zipf(1.1)/0.05% frontier)"),
+    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=8192, sweep=True,
+                    desc="C3: Mastic(BITS=256, Count) weighted heavy hitters, full 256-level threshold-pruned "
+                         "sweep (Zipf(1.1) over 2^20 random 256-bit strings, threshold 0.05% of all reports), "
+                         "both aggregators per level; run with --steps 1 --warmup 0"),
     "c4": dict(circuit="Histogram", kw=dict(bits=64, length=64, chunk_length=8), prefixes=1000, reports=12288,
                desc="C4: Mastic(BITS=64, Histogram length=64 chunk 8, Field128) prep_init+aggregate, level 63"),
     "c5": dict(circuit="SumVec", kw=dict(bits=32, length=1024, sum_vec_bits=1, chunk_length=32), prefixes=100,
@@ -153,6 +157,151 @@ def cpu_baseline(jobs, procs):
     return wall, res
 
 
+# ---------------------------------------------------------------- C3 sweep
+def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
+    """BASELINE config C3: the reference's heavy-hitters driver (examples.py:37-91,
+    mastic_amd.heavy_hitters) over HBM-resident reports, each rank sweeping its
+    shard and merging every level's agg shares over RCCL before pruning.
+    A step = one full 256-level sweep (both aggregators' prep_init, decide,
+    fold and merge at every level).  Units = sum over levels and aggregators
+    of reports x candidate prefixes."""
+    from mastic_amd import Mastic
+    from mastic_amd.heavy_hitters import compute_heavy_hitters
+    from mastic_amd.merge import merge_field_shares
+
+    kw = dict(cfg["kw"])
+    bits = kw.pop("bits")
+    m = Mastic(bits, cfg["circuit"], device=local, **kw)
+    ctx = b"mastic-mi355x-bench"
+    seed = 0x4D41 + 3
+    pool = np.random.default_rng(seed).integers(0, 256, size=(2 ** 20, bits // 8), dtype=np.uint8)
+    rrng = np.random.default_rng(seed * 1000003 + rank)
+    ranks = rrng.zipf(1.1, size=n_rep)
+    while (ranks > len(pool)).any():
+        bad = ranks > len(pool)
+        ranks[bad] = rrng.zipf(1.1, size=int(bad.sum()))
+    alpha_b = pool[ranks - 1].tobytes()
+    betas = np.ones(n_rep, dtype="<u8").tobytes()
+    nonces = rrng.integers(0, 256, size=16 * n_rep, dtype=np.uint8).tobytes()
+    rands = rrng.integers(0, 256, size=m.RAND_SIZE * n_rep, dtype=np.uint8).tobytes()
+    reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
+    vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
+    thresholds = {"default": max(1, int(np.ceil(0.0005 * n_rep * world)))}
+    merge = merge_field_shares(m, dist) if dist else None
+
+    def step(trace, timing):
+        return compute_heavy_hitters(m, ctx, thresholds, reps, verify_key=vk, trace=trace, merge=merge,
+                                     timing=timing)
+
+    for _ in range(args.warmup):
+        step(None, None)
+    m.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    traces, timing = [], []
+    hh = None
+    for _ in range(args.steps):
+        tr = []
+        hh = step(tr, timing)
+        traces.append(tr)
+    m.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    units = sum(2 * n_rep * len(lv.prefixes) for tr in traces for lv in tr) * world
+    nodes = 0
+    for lv in traces[0]:
+        if lv.prefixes:
+            nodes += m.tree_stats((lv.level, tuple(lv.prefixes), lv.level == 0))[0]
+    nodes *= 2 * n_rep * args.steps  # both aggregators
+    aes_per_node = 1 + (16 + m.VALUE_LEN * m.field.ENCODED_SIZE + 15) // 16
+    dom_ops = aes_per_node * AES_BLOCK_OPS + 2 * m.VALUE_LEN * FIELD_ADD_OPS + KECCAK_OPS
+    dom_ms = sum(t[0] + t[2] for t in timing)
+    n_launch = sum(t[1] for t in timing)
+    achieved = nodes * dom_ops / (dom_ms / 1e3) / 1e12 if dom_ms > 0 else 0.0
+    widths = [len(lv.prefixes) for lv in traces[0]]
+    out = {
+        "metric": METRIC,
+        "value": units / dt,
+        "unit": "report*prefix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {
+            "workload": "%s, %d reports per rank" % (cfg["desc"], n_rep),
+            "reports_per_step": n_rep * world,
+            "threshold": thresholds["default"],
+            "levels": len(traces[0]),
+            "max_candidates_per_level": max(widths),
+            "sum_candidates_over_levels": sum(widths),
+            "heavy_hitters": len(hh),
+            "node_evals_per_step": nodes // args.steps,
+            "field": "Field64",
+            "parallelism": "reports sharded %d-way, per-level agg-share all-gather + GPU fold" % world,
+        },
+        "roofline": {
+            "kernel": "k_eval_aes<F64> (+ node-proof waves, + k_node_proof for the last level)",
+            "bound": "valu",
+            "achieved": achieved,
+            "peak": VALU_PEAK_TOPS,
+            "unit": "Tops/s (int32)",
+            "frac": achieved / VALU_PEAK_TOPS,
+            "traffic": None,
+            "launches": n_launch,
+            "avg_launch_ms": dom_ms / max(n_launch, 1),
+            "ops_per_node": dom_ops,
+        },
+        "breakdown_ms_per_step": {
+            "eval_aes_plus_proofs": dom_ms / args.steps,
+            "absorb": sum(t[4] for t in timing) / args.steps,
+            "prep_init_total": sum(t[6] for t in timing) / args.steps,
+        },
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        # oracle prep_init (leader) of one report per process at 8 levels spread over the sweep,
+        # with the GPU trace's candidate prefixes: a bounded sample of the same workload
+        procs = min(args.cpu_procs, os.cpu_count() or 1)
+        lvls = [lv for lv in traces[0] if lv.prefixes][::max(1, len(traces[0]) // 8)][:8]
+        (rn, pub, in0, _in1) = reps.download()
+        ps, isz = m.sizes.public_share_size, m.sizes.input_share_size[0]
+        spec = (cfg["circuit"], cfg["kw"])
+        jobs = []
+        for i in range(procs):
+            for lv in lvls:
+                enc_ap = m.encode_agg_param((lv.level, tuple(lv.prefixes), lv.level == 0))
+                jobs.append((spec, enc_ap, rn[16 * i:16 * (i + 1)], pub[ps * i:ps * (i + 1)],
+                             in0[isz * i:isz * (i + 1)], vk, ctx, 0))
+        wall, res = cpu_baseline(jobs, procs)
+        cu = procs * sum(len(lv.prefixes) for lv in lvls)
+        out["cpu_baseline"] = {
+            "value": cu / wall,
+            "unit": "report*prefix/s",
+            "cores": procs,
+            "kind": "port",
+            "sample": "%d reports (one per process, spawn pool of %d) x leader prep_init at levels %s of the "
+                      "sweep with the GPU run's candidate prefixes; poc-faithful Python oracle with C "
+                      "AES/TurboSHAKE" % (procs, procs, [lv.level for lv in lvls]),
+        }
+    if rank == 0:
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
@@ -170,6 +319,8 @@ def main():
 
     cfg = CONFIGS[args.config]
     n_rep = args.reports or cfg["reports"]
+    if cfg.get("sweep"):
+        return run_sweep(args, cfg, n_rep, world, rank, local, dist, torch)
     n_pre = args.prefixes or cfg["prefixes"]
     kw = dict(cfg["kw"])
     bits = kw.pop("bits")

@@ -14,6 +14,10 @@ what is computed:
     at ``prep_shares_to_prep``) is dropped from that level's aggregate and
     from every later level, which is what a deployed aggregator does.  With
     only honest reports the output is identical to the reference's.
+  * multi-GPU: every rank sweeps its own shard of
+    the reports and passes ``merge`` (e.g. :func:`mastic_amd.merge.merge_field_shares`:
+    RCCL all-gather + GPU mod-p fold), so each level's pruning decision is
+    taken on the job-wide aggregate and all ranks walk the same frontier.
 """
 import numpy as np
 
@@ -24,6 +28,8 @@ def get_threshold(thresholds, prefix):
     """poc/examples.py:26-34: the threshold of the longest proper prefix of
     ``prefix`` listed in ``thresholds`` (the prefix itself excluded), else
     ``thresholds['default']``."""
+    if len(thresholds) == 1:  # only 'default' (common case: skips the O(len) walk)
+        return thresholds['default']
     for level in reversed(range(len(prefix) - 1)):
         if prefix[:level + 1] in thresholds:
             return thresholds[prefix[:level + 1]]
@@ -49,7 +55,7 @@ class SweepLevel:
 
 
 def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verify_key: bytes = None,
-                          trace=None):
+                          trace=None, merge=None, timing=None):
     """poc/examples.py:37-91 on the GPU.
 
     ``reports`` is either the reference's list of
@@ -57,7 +63,10 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     :class:`~mastic_amd.vdaf.Reports` batch holding both input shares
     (``Mastic.reports_shard`` / ``reports_upload``).  ``verify_key`` defaults
     to fresh randomness, as in the reference.  If ``trace`` is a list, one
-    :class:`SweepLevel` per level is appended to it.
+    :class:`SweepLevel` per level is appended to it.  ``merge`` maps this
+    rank's agg share (list of field elements) to the job-wide one (all
+    ranks call it at every level, in the same order).  If ``timing`` is a
+    list, ``mastic.last_timing3()`` of every prep_init is appended to it.
     """
     if verify_key is None:
         import os
@@ -79,18 +88,23 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     for level in range(bits):
         agg_param = (level, tuple(prefixes), level == 0)
         assert mastic.is_valid(agg_param, prev_agg_params)
+        enc = mastic.encode_agg_param(agg_param)  # once per level: the batch calls take the encoding
 
         if n and prefixes:
             shares = []
             for agg_id in range(2):
-                mastic.prep_init_device(dev, verify_key, ctx, agg_id, agg_param)
-                shares.append(mastic.prep_result(dev, agg_id, agg_param))
-            (_msgs, valid) = mastic.decide_batch(ctx, agg_param, shares[0][0], shares[1][0])
+                mastic.prep_init_device(dev, verify_key, ctx, agg_id, enc)
+                shares.append(mastic.prep_result(dev, agg_id, enc))
+                if timing is not None:
+                    timing.append(mastic.last_timing3())
+            (_msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
             alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
             mask = alive.astype(np.uint8)
-            agg_shares = [mastic.aggregate_device(agg_id, agg_param, mask) for agg_id in range(2)]
+            agg_shares = [mastic.aggregate_device(agg_id, enc, mask) for agg_id in range(2)]
         else:
             agg_shares = [mastic.agg_init(agg_param) for _ in range(2)]
+        if merge is not None:
+            agg_shares = [merge(a) for a in agg_shares]
         agg_result = mastic.unshard(agg_param, agg_shares, int(alive.sum()))
         prev_agg_params.append(agg_param)
         if trace is not None:

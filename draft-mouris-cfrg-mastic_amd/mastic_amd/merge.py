@@ -40,3 +40,14 @@ def merge_agg_shares(m, agg_share, dist):
     local = torch.frombuffer(bytearray(m.field.encode_vec(agg_share)), dtype=torch.uint8).cuda()
     gathered = gather_shares(local, dist)
     return fold_on_gpu(m, gathered, dist.get_world_size(), len(agg_share))
+
+
+def merge_field_shares(m, dist):
+    """``merge`` callback for the sweep driver (heavy_hitters.compute_heavy_hitters):
+    rank-local agg share -> job-wide agg share, both as lists of field elements."""
+    def merge(agg_share):
+        if len(agg_share) == 0:
+            return agg_share
+        merged = merge_agg_shares(m, agg_share, dist)
+        return m.field.decode_vec(merged.cpu().numpy().tobytes())
+    return merge

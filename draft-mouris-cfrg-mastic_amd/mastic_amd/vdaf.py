@@ -31,10 +31,7 @@ def _check(ctx_ptr, rc):
 
 def _pack_path(path) -> bytes:
     """MSB-first bit packing (PrefixTreeIndex.encode, poc/vidpf.py:33-39)."""
-    out = bytearray((len(path) + 7) // 8)
-    for (i, b) in enumerate(path):
-        out[i // 8] |= int(bool(b)) << (7 - i % 8)
-    return bytes(out)
+    return np.packbits(np.fromiter(path, dtype=bool, count=len(path))).tobytes()
 
 
 def _pack_bits_lsb(bits) -> bytes:

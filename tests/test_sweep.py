@@ -64,6 +64,9 @@ class _StubMastic:
         wc = (agg_param[2] and not prev) or (not agg_param[2] and any(p[2] for p in prev))
         return wc and (not prev or agg_param[0] > prev[-1][0])
 
+    def encode_agg_param(self, agg_param):
+        return agg_param  # the stub's batch calls take the tuple itself
+
     def prep_init_device(self, dev, vk, ctx, agg_id, agg_param):
         self.calls.append((agg_id, agg_param[0], len(agg_param[1])))
         self._dev, self._ap = dev, agg_param
