@@ -30,6 +30,9 @@ KECCAK_OPS = 3720
 FIELD_ADD_OPS = 4
 # int32 VALU peak: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# full-rate int32 VALU throughput measured on an MI355X at the clock it holds under load
+# (v_bitop3_b32, 8 waves/SIMD: tools/valu_peak.hip, profiles/r01_v9_valu_peak.json)
+VALU_MEASURED_TOPS = 67.9
 HBM_PEAK_GBS = 8000.0
 
 
@@ -260,6 +263,8 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "peak": VALU_PEAK_TOPS,
             "unit": "Tops/s (int32)",
             "frac": achieved / VALU_PEAK_TOPS,
+            "peak_measured": VALU_MEASURED_TOPS,
+            "frac_of_measured_peak": achieved / VALU_MEASURED_TOPS,
             "traffic": None,
             "launches": n_launch,
             "avg_launch_ms": dom_ms / max(n_launch, 1),
@@ -413,6 +418,8 @@ def main():
             "peak": VALU_PEAK_TOPS,
             "unit": "Tops/s (int32)",
             "frac": achieved / VALU_PEAK_TOPS,
+            "peak_measured": VALU_MEASURED_TOPS,
+            "frac_of_measured_peak": achieved / VALU_MEASURED_TOPS,
             "traffic": None,
             "launches": n_launch,
             "avg_launch_ms": dom_ms / max(n_launch, 1),
