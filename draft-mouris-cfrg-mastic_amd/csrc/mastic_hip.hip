@@ -264,6 +264,9 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
     if (len != 6 + plen * count + 1) return fail(c, MASTIC_EINVAL, "agg param has incorrect length");
     if (level >= c->p.bits) return fail(c, MASTIC_EINVAL, "level too deep");
     if (enc[len - 1] > 1) return fail(c, MASTIC_EINVAL, "invalid weight check flag");
+    // the poc cannot evaluate an empty candidate set either (eval_with_siblings leaves the
+    // root's children unset and prep_init fails at mastic.py:270)
+    if (count == 0) return fail(c, MASTIC_EINVAL, "empty candidate prefix list");
     const uint8_t* pre = enc + 6;
     // prefixes as MSB-first byte strings of plen bytes (bits past level+1 must be zero)
     const int tail_bits = (level + 1) % 8;

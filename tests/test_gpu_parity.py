@@ -379,3 +379,68 @@ def test_fast_path_handover_field128(mastic_amd, blk, monkeypatch):
     vk = bytes(rng.getrandbits(8) for _ in range(32))
     ap = _random_agg_param(m, rng, alphas, 4, 5, True)
     _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=False)
+
+
+# ------------------------------------------------------------ edge cases
+def test_empty_batch(mastic_amd):
+    """Zero reports: empty outputs and an all-zero aggregate (agg_init)."""
+    m = mastic_amd.MasticSum(6, 7)
+    ap = (5, ((True,) * 6, (False,) * 6), True)
+    (ps, js, out, st) = m.prep_init_batch(bytes(32), CTX, 0, ap, b"", b"", b"")
+    assert ps == b"" and len(st) == 0
+    agg = m.aggregate_device(0, ap)
+    assert [x.int() for x in agg] == [0] * (2 * (1 + m.OUTPUT_LEN))
+
+
+def test_empty_prefix_list_rejected(mastic_amd):
+    """The poc cannot evaluate an empty candidate set (mastic.py:270 reads the
+    root's unset children); the GPU path refuses it with ValueError."""
+    rng = random.Random(21)
+    m = mastic_amd.MasticCount(4)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 2)
+    (pub, in0, _in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    for level in (0, 3):
+        with pytest.raises(ValueError):
+            m.prep_init_batch(bytes(32), CTX, 0, (level, (), True), nonces, pub, in0)
+
+
+@pytest.mark.parametrize("n", [1, 63, 65])
+def test_ragged_batch_sizes(mastic_amd, n):
+    """Batches that do not fill whole 64-report groups: every report of the
+    batch bit-exact against the oracle (padding lanes must not leak)."""
+    rng = random.Random(300 + n)
+    m = mastic_amd.MasticSum(5, 3)
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, n)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    ap = _random_agg_param(m, rng, alphas, 4, 6, True)
+    _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=(n == 1))
+
+
+def test_max_bits_many_prefixes_properties(mastic_amd):
+    """BITS 256 (the largest BASELINE config) at level 255 with 512 candidates:
+    both aggregators agree (decide), and the aggregate equals the plaintext
+    counts (talks/func.py:49-80)."""
+    rng = random.Random(31)
+    m = mastic_amd.MasticCount(256)
+    n = 96
+    pool = [tuple(bool(rng.getrandbits(1)) for _ in range(256)) for _ in range(24)]
+    alphas = [pool[rng.randrange(len(pool))] for _ in range(n)]
+    weights = [rng.randrange(2) for _ in range(n)]
+    nonces = bytes(rng.getrandbits(8) for _ in range(16 * n))
+    rands = bytes(rng.getrandbits(8) for _ in range(m.RAND_SIZE * n))
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    cand = set(pool)
+    while len(cand) < 512:
+        cand.add(tuple(bool(rng.getrandbits(1)) for _ in range(256)))
+    ap = (255, tuple(sorted(cand)), True)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    res = [m.prep_init_batch(vk, CTX, a, ap, nonces, pub, in0 if a == 0 else in1, want_out_shares=False)
+           for a in range(2)]
+    (_msgs, valid) = m.decide_batch(CTX, ap, res[0][0], res[1][0])
+    assert list(valid) == [1] * n
+    aggs = [m.aggregate_device(a, ap) for a in range(2)]
+    want = {}
+    for (a, w) in zip(alphas, weights):
+        want[a] = want.get(a, 0) + w
+    assert m.unshard(ap, aggs, n) == [want.get(p, 0) for p in ap[1]]
