@@ -39,6 +39,7 @@ enum PfxId {
     PFX_JR_SEED,        // joint rand seed, empty seed
     PFX_JR,             // joint rand, 32-byte seed follows
     PFX_PROVE_RAND,     // prove rand (client), 32-byte seed follows
+    PFX_TREE,           // eval-proof Merkle tree node hash (proof-aggregation mode), empty seed
     PFX_COUNT
 };
 
@@ -1186,6 +1187,43 @@ __global__ __launch_bounds__(256) void k_fold_shares(const uint32_t* in, int n_s
         acc = F::add(acc, F::from_words(w));
     }
     for (int i = 0; i < F::W32; i++) out[(size_t)e * F::W32 + i] = F::word(acc, i);
+}
+
+// ------------------------------------------------------------- proof tree
+// VIDPF-proof aggregation mode (draft-mouris-cfrg-mastic.md, "Plain
+// Heavy-Hitters with VIDPF-Proof Aggregation"): the aggregators compute
+// identical eval proofs iff a report is valid, so they compare Merkle trees
+// over the batch's eval proofs instead of exchanging every prep share, and
+// descend into differing subtrees to isolate invalid reports.  The draft
+// leaves the hash unspecified; here a node of two children is
+//   XofTurboShake128(b'', dst(ctx, USAGE_PROOF_TREE = 12), left || right).next(32)
+// and the last node of an odd level is promoted unchanged.  Nodes are 32-byte
+// rows (node-major), levels concatenated leaves first.
+__global__ __launch_bounds__(256) void k_proof_tree_leaves(const uint32_t* eval_proof, int n, int stride,
+                                                          uint32_t* leaves) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+#pragma unroll
+    for (int j = 0; j < 8; j++) leaves[(size_t)i * 8 + j] = eval_proof[(size_t)j * stride + i];
+}
+
+__global__ __launch_bounds__(256) void k_proof_tree_level(const PrefixState* pfx, const uint32_t* in, int n_in,
+                                                         uint32_t* out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n_out = (n_in + 1) >> 1;
+    if (i >= n_out) return;
+    const uint32_t* lr = in + (size_t)(2 * i) * 8;  // left || right: 16 consecutive words
+    if (2 * i + 1 >= n_in) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) out[(size_t)i * 8 + j] = lr[j];
+        return;
+    }
+    KState s;
+    int f;
+    load_prefix(pfx, PFX_TREE, s, f);
+    f = sponge_absorb_words(s, f, 64, [&](int m) { return lr[m]; });
+    sponge_pad(s, f, 0x01);
+    sponge_squeeze_words(s, 8, [&](int j, uint32_t w) { out[(size_t)i * 8 + j] = w; });
 }
 
 // ------------------------------------------------------------- decide

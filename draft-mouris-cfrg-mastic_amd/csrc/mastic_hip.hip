@@ -201,6 +201,7 @@ static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len,
     xof_ts(PFX_JR_SEED, dst_alg(app_ctx, ctx_len, 3, ID), 0, nullptr);
     xof_ts(PFX_JR, dst_alg(app_ctx, ctx_len, 5, ID), 32, nullptr);
     xof_ts(PFX_PROVE_RAND, dst_alg(app_ctx, ctx_len, 0, ID), 32, nullptr);
+    xof_ts(PFX_TREE, dst(app_ctx, ctx_len, 12), 0, nullptr);
     std::vector<uint8_t> all;
     std::vector<int> meta(2 * PFX_COUNT);
     for (int i = 0; i < PFX_COUNT; i++) {
@@ -878,6 +879,40 @@ extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t 
         hipLaunchKernelGGL(k_fold_shares<F128>, grid, dim3(256), 0, c->stream, (const uint32_t*)dev_shares,
                            (int)n_shares, (int)n_elems, (uint32_t*)dev_out);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Eval-proof Merkle tree (proof-aggregation mode, kernels.hpp k_proof_tree_*)
+// over the last prep_init result of agg_id.
+extern "C" int mastic_proof_tree(mastic_ctx* c, int agg_id, const uint8_t* app_ctx, size_t ctx_len,
+                                 uint8_t* nodes_out, size_t n_nodes) {
+    DeviceScope ds_(c);
+    if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
+    Result& R = c->res[agg_id];
+    if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
+    const size_t n = R.n;
+    size_t total = 0;
+    for (size_t m = n; m > 0; m = (m == 1) ? 0 : (m + 1) / 2) total += m;
+    if (n_nodes != total) return fail(c, MASTIC_EINVAL, "proof tree has incorrect size");
+    if (n == 0) return 0;
+    if (n > (size_t)INT32_MAX / 2) return fail(c, MASTIC_EINVAL, "batch too large for a proof tree");
+    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr);
+    if (rc) return rc;
+    DevBuf nodes;
+    if (!nodes.ensure(total * 32)) return fail(c, MASTIC_ENOMEM, "out of device memory (proof tree)");
+    uint32_t* d = nodes.as<uint32_t>();
+    hipLaunchKernelGGL(k_proof_tree_leaves, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
+                       R.eval_proof.as<uint32_t>(), (int)n, (int)R.stride, d);
+    size_t off = 0;
+    for (size_t m = n; m > 1; m = (m + 1) / 2) {
+        const size_t mo = (m + 1) / 2;
+        hipLaunchKernelGGL(k_proof_tree_level, dim3((unsigned)((mo + 255) / 256)), dim3(256), 0, c->stream,
+                           (const PrefixState*)c->pfx.p, d + off * 8, (int)m, d + (off + m) * 8);
+        off += m;
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(nodes_out, d, total * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }

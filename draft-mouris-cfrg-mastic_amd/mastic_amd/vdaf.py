@@ -296,6 +296,21 @@ class Mastic:
                                                        ctypes.byref(b), ctypes.byref(c)))
         return (a.value, b.value, c.value)
 
+    def proof_tree(self, agg_id: int, ctx: bytes, n: int):
+        """Merkle tree over the eval proofs of the last prep_init of agg_id
+        over n reports (proof-aggregation mode, see mastic_amd.proof_agg):
+        list of levels, leaves first, each a list of 32-byte nodes."""
+        from .proof_agg import level_sizes
+        sizes = level_sizes(n)
+        out = np.empty(32 * max(1, sum(sizes)), np.uint8)
+        _check(self._ctx, _lib.lib().mastic_proof_tree(self._ctx, agg_id, ctx, len(ctx), _lib.buf(out), sum(sizes)))
+        raw = out.tobytes()
+        levels, off = [], 0
+        for m in sizes:
+            levels.append([raw[32 * (off + i):32 * (off + i + 1)] for i in range(m)])
+            off += m
+        return levels
+
     def work_bytes(self, agg_param):
         """HBM work bytes per report of one prep_init at this agg param
         (batches larger than the memory budget allows are run in chunks)."""

@@ -130,6 +130,17 @@ int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t*
  * output of an RCCL all-gather): dev_out[e] = sum_s dev_shares[s][e] mod p.
  * Elements are in encode_vec byte order. */
 int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares, size_t n_elems, void* dev_out);
+/* VIDPF-proof aggregation mode (draft-mouris-cfrg-mastic.md, "Plain
+ * Heavy-Hitters with VIDPF-Proof Aggregation"; no poc code or wire format in
+ * the reference): Merkle tree over the eval proofs of the last prep_init of
+ * agg_id.  Leaves = the n eval proofs (32 B each, report order); a node of two
+ * children = XofTurboShake128(b"", dst(app_ctx, 12), left || right).next(32);
+ * the last node of an odd level is promoted unchanged.  nodes_out receives
+ * all levels, leaves first, 32 B per node; n_nodes must equal
+ * n + ceil(n/2) + ... + 1 (0 for n = 0).  Both aggregators' roots are equal iff
+ * every report's eval proofs agree (mastic.py:340). */
+int mastic_proof_tree(mastic_ctx* ctx, int agg_id, const uint8_t* app_ctx, size_t ctx_len, uint8_t* nodes_out,
+                      size_t n_nodes);
 /* Wait for all enqueued work of the ctx. */
 int mastic_synchronize(mastic_ctx* ctx);
 
