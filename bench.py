@@ -45,7 +45,7 @@ CONFIGS = {
     "c3": dict(circuit="Count", kw=dict(bits=256), prefixes=128, reports=16384,
                desc="C3: Mastic(BITS=256, Count) prep_init+aggregate at level 255 of the threshold-pruned "
                     "sweep (128 surviving candidates, the Zipf(1.1)/0.05% frontier)"),
-    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=8192, sweep=True,
+    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=16384, sweep=True,
                     desc="C3: Mastic(BITS=256, Count) weighted heavy hitters, full 256-level threshold-pruned "
                          "sweep (Zipf(1.1) over 2^20 random 256-bit strings, threshold 0.05% of all reports), "
                          "both aggregators per level; run with --steps 1 --warmup 0"),
