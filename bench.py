@@ -340,7 +340,7 @@ def main():
 
     def step():
         m.prep_init_device(reps, vk, ctx, args.agg_id, enc_ap)
-        agg = m.aggregate_device(args.agg_id, enc_ap)
+        agg = m.aggregate_device(args.agg_id, enc_ap, raw=True)
         if world > 1:
             merge_agg_shares(m, agg, dist)  # RCCL all-gather + on-GPU mod-p fold
         return agg

@@ -34,12 +34,13 @@ def fold_on_gpu(m, gathered, world, n_elems):
 
 
 def merge_agg_shares(m, agg_share, dist):
-    """Rank-local agg share (list of field elements) -> job-wide agg share
-    (uint8 device tensor in encode_vec order) on every rank."""
+    """Rank-local agg share (list of field elements, or its encode_vec bytes)
+    -> job-wide agg share (uint8 device tensor in encode_vec order) on every rank."""
     import torch
-    local = torch.frombuffer(bytearray(m.field.encode_vec(agg_share)), dtype=torch.uint8).cuda()
+    raw = bytes(agg_share) if isinstance(agg_share, (bytes, bytearray)) else m.field.encode_vec(agg_share)
+    local = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
     gathered = gather_shares(local, dist)
-    return fold_on_gpu(m, gathered, dist.get_world_size(), len(agg_share))
+    return fold_on_gpu(m, gathered, dist.get_world_size(), len(raw) // m.field.ENCODED_SIZE)
 
 
 def merge_field_shares(m, dist):

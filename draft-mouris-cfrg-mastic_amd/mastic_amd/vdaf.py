@@ -223,14 +223,15 @@ class Mastic:
             _lib.buf(msgs), _lib.buf(valid)))
         return (msgs.tobytes(), valid)
 
-    def aggregate_device(self, agg_id: int, agg_param, valid=None):
-        """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU."""
+    def aggregate_device(self, agg_id: int, agg_param, valid=None, raw=False):
+        """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU
+        (raw=True: the agg share as encode_vec bytes, without decoding)."""
         enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
         (_level, count, _wc) = self._agg_param_header(enc)
         out = np.empty(count * (1 + self.OUTPUT_LEN) * self.field.ENCODED_SIZE, np.uint8)
         v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
         _check(self._ctx, _lib.lib().mastic_aggregate(self._ctx, agg_id, _lib.buf(v), _lib.buf(out)))
-        return self.field.decode_vec(out.tobytes())
+        return out.tobytes() if raw else self.field.decode_vec(out.tobytes())
 
     # ------------------------------------------- device-resident batches
     def reports_shard(self, ctx: bytes, alphas_packed: bytes, betas: bytes, nonces: bytes, rands: bytes):
