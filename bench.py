@@ -45,7 +45,13 @@ CONFIGS = {
     "c3": dict(circuit="Count", kw=dict(bits=256), prefixes=128, reports=16384,
                desc="C3: Mastic(BITS=256, Count) prep_init+aggregate at level 255 of the threshold-pruned "
                     "sweep (128 surviving candidates, the Zipf(1.1)/0.05% frontier)"),
-    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=16384, sweep=True,
+    "c1sweep": dict(circuit="Count", kw=dict(bits=16), prefixes=0, reports=1000, sweep=True, pool=128, zipf=1.2,
+                    weight_p=0.9, threshold=10,
+                    desc="C1: Mastic(BITS=16, Count) weighted heavy hitters, full 16-level sweep (Zipf(1.2) over "
+                         "128 random 16-bit strings, weights Bernoulli(0.9), threshold 10), both aggregators per "
+                         "level: the reference's CPU-sized case"),
+    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=16384, sweep=True, pool=2 ** 20, zipf=1.1,
+                    weight_p=1.0, threshold=None,
                     desc="C3: Mastic(BITS=256, Count) weighted heavy hitters, full 256-level threshold-pruned "
                          "sweep (Zipf(1.1) over 2^20 random 256-bit strings, threshold 0.05% of all reports), "
                          "both aggregators per level; run with --steps 1 --warmup 0"),
@@ -162,12 +168,12 @@ def cpu_baseline(jobs, procs):
 
 # ---------------------------------------------------------------- C3 sweep
 def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
-    """BASELINE config C3: the reference's heavy-hitters driver (examples.py:37-91,
-    mastic_amd.heavy_hitters) over HBM-resident reports, each rank sweeping its
-    shard and merging every level's agg shares over RCCL before pruning.
-    A step = one full 256-level sweep (both aggregators' prep_init, decide,
-    fold and merge at every level).  Units = sum over levels and aggregators
-    of reports x candidate prefixes."""
+    """BASELINE configs C1 and C3: the reference's heavy-hitters driver
+    (examples.py:37-91, mastic_amd.heavy_hitters) over HBM-resident reports,
+    each rank sweeping its shard and merging every level's agg shares over
+    RCCL before pruning.  A step = one full level sweep (both aggregators'
+    prep_init, decide, fold and merge at every level).  Units = sum over
+    levels and aggregators of reports x candidate prefixes."""
     from mastic_amd import Mastic
     from mastic_amd.heavy_hitters import compute_heavy_hitters
     from mastic_amd.merge import merge_field_shares
@@ -176,20 +182,20 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
     bits = kw.pop("bits")
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
     ctx = b"mastic-mi355x-bench"
-    seed = 0x4D41 + 3
-    pool = np.random.default_rng(seed).integers(0, 256, size=(2 ** 20, bits // 8), dtype=np.uint8)
+    seed = 0x4D41 + int(args.config[1])
+    pool = np.random.default_rng(seed).integers(0, 256, size=(cfg["pool"], bits // 8), dtype=np.uint8)
     rrng = np.random.default_rng(seed * 1000003 + rank)
-    ranks = rrng.zipf(1.1, size=n_rep)
+    ranks = rrng.zipf(cfg["zipf"], size=n_rep)
     while (ranks > len(pool)).any():
         bad = ranks > len(pool)
-        ranks[bad] = rrng.zipf(1.1, size=int(bad.sum()))
+        ranks[bad] = rrng.zipf(cfg["zipf"], size=int(bad.sum()))
     alpha_b = pool[ranks - 1].tobytes()
-    betas = np.ones(n_rep, dtype="<u8").tobytes()
+    betas = (rrng.random(n_rep) < cfg["weight_p"]).astype("<u8").tobytes()
     nonces = rrng.integers(0, 256, size=16 * n_rep, dtype=np.uint8).tobytes()
     rands = rrng.integers(0, 256, size=m.RAND_SIZE * n_rep, dtype=np.uint8).tobytes()
     reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
     vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
-    thresholds = {"default": max(1, int(np.ceil(0.0005 * n_rep * world)))}
+    thresholds = {"default": cfg["threshold"] or max(1, int(np.ceil(0.0005 * n_rep * world)))}
     merge = merge_field_shares(m, dist) if dist else None
 
     def step(trace, timing):
