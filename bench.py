@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--agg-id", type=int, default=0)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU baseline leg")
     ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--frontier-cache", type=int, default=1,
+                    help="sweep configs: keep each level's binder inputs in HBM (Mastic.set_frontier_cache)")
     return ap.parse_args()
 
 
@@ -198,9 +200,13 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
     thresholds = {"default": cfg["threshold"] or max(1, int(np.ceil(0.0005 * n_rep * world)))}
     merge = merge_field_shares(m, dist) if dist else None
 
+    cached_levels = []
+
     def step(trace, timing):
+        cached_levels.clear()
         return compute_heavy_hitters(m, ctx, thresholds, reps, verify_key=vk, trace=trace, merge=merge,
-                                     timing=timing)
+                                     timing=timing, frontier_cache=bool(args.frontier_cache),
+                                     cached_levels=cached_levels)
 
     for _ in range(args.warmup):
         step(None, None)
@@ -226,9 +232,16 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
         dt = float(tt.item())
 
     units = sum(2 * n_rep * len(lv.prefixes) for tr in traces for lv in tr) * world
+    # node evaluations actually performed: a level served from the frontier cache evaluates
+    # only its new tree level (both children of every distinct length-L prefix)
+    hit = set(cached_levels)
     nodes = 0
     for lv in traces[0]:
-        if lv.prefixes:
+        if not lv.prefixes:
+            continue
+        if lv.level in hit:
+            nodes += 2 * len(set(p[:lv.level] for p in lv.prefixes))
+        else:
             nodes += m.tree_stats((lv.level, tuple(lv.prefixes), lv.level == 0))[0]
     nodes *= 2 * n_rep * args.steps  # both aggregators
     aes_per_node = 1 + (16 + m.VALUE_LEN * m.field.ENCODED_SIZE + 15) // 16
@@ -258,6 +271,8 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "max_candidates_per_level": max(widths),
             "sum_candidates_over_levels": sum(widths),
             "heavy_hitters": len(hh),
+            "frontier_cache": bool(args.frontier_cache),
+            "levels_evaluated_from_cache": len(cached_levels),
             "node_evals_per_step": nodes // args.steps,
             "field": "Field64",
             "parallelism": "reports sharded %d-way, per-level agg-share all-gather + GPU fold" % world,

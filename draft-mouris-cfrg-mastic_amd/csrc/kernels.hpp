@@ -488,6 +488,11 @@ struct AesArgs {
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
     int force_slow_blk;  // test hook: the Field64 fast path hands over to the exact stream at this block (-1 = never)
+    // frontier cache (mastic_set_frontier_cache): payloads of ALL children of this level by child
+    // node index (the last level of a prep_init, read back as the parents' payloads next call), and
+    // fr_w_in indexed by the parent's node index (parent_node) instead of its ordinal
+    uint32_t* last_w;
+    int wp_by_node;
     // node proofs of the PREVIOUS level (vidpf.py:366-380, :321-323), computed
     // by the workgroup's EVAL_PROOF_WAVES proof waves beside the AES waves
     int pv_level;                   // level - 1
@@ -685,6 +690,10 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             if (tc1) x1 = F::add(x1, cw);
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
+            if (a.last_w) {
+                pl_store<F>(a.last_w, (2 * pi) * vl + e, S, r, x0);
+                pl_store<F>(a.last_w, (2 * pi + 1) * vl + e, S, r, x1);
+            }
             if (l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
@@ -720,7 +729,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             }
         };
         auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
-        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, pi * vl + e, S, r) : F::zero(); };
+        const int wpi = a.wp_by_node ? a.parent_node[pi] : pi;
+        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, wpi * vl + e, S, r) : F::zero(); };
         int e_fast = 0;  // elements completed by the fast path
         if constexpr (!QUAD) {
             // Fast path: block b (counter b + 1) of each child's convert stream

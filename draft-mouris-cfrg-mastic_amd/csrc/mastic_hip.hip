@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -67,11 +68,36 @@ struct Result {
 
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
+// Frontier cache of one aggregator (mastic_set_frontier_cache; SURVEY.md §8f
+// row 1).  In a level sweep (examples.py:37-91) prep_init at level L evaluates
+// the whole tree again, but its levels 0..L-1 are usually exactly the previous
+// call's tree.  The cache keeps, per report, every level's node proofs and
+// payload differences (the binder inputs, tiled as in the ring buffers), the
+// last level's child seeds / control bits and payloads, and the root sum;
+// a call whose tree extends the cached one by one level evaluates only that
+// level and re-absorbs the rest from the cache.
+struct LevelCache {
+    bool valid = false;
+    uint64_t rep_gen = 0;
+    size_t n = 0;
+    int stride = 0;
+    std::vector<uint8_t> key;                   // verify key || ctx
+    int L = -1;                                 // level of the cached call
+    std::vector<int> n_parents;                 // per level 0..L
+    std::vector<uint32_t> paths;                // child paths of levels 0..L (8 words per node)
+    std::vector<std::unique_ptr<DevBuf>> oh, pay;  // per level: proofs tile, payload-difference tile
+    DevBuf cs[2], w[2], rootsum;                // last level's seeds/ctrl and payloads; root sum
+    int wcur = 0;                               // which cs / w hold the cached level (the other is written)
+    void drop() { valid = false; }
+};
+
 }  // namespace
 
+static uint64_t g_reports_gen = 0;  // contents generation (frontier-cache key)
 struct mastic_reports {
     mastic_ctx* ctx = nullptr;
     size_t n = 0;
+    uint64_t gen = ++g_reports_gen;
     DevBuf nonces, pub, in0, in1;
 };
 
@@ -106,6 +132,9 @@ struct mastic_ctx {
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
+    bool frontier_cache = false;  // mastic_set_frontier_cache
+    bool last_hit = false;        // the last prep_init evaluated only its last level
+    LevelCache lc[2];
     // timing
     std::vector<hipEvent_t> ev;
     double t_eval = 0, t_proof = 0, t_absorb = 0, t_total = 0;
@@ -523,7 +552,7 @@ static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst
 
 template <class F>
 static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
-                     size_t base, int n, int stride, size_t& evi) {
+                     size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit) {
     const McParams& p = c->p;
     uint32_t* W = c->work.as<uint32_t>();
     Planes pl = make_planes(W, wl, n, stride);
@@ -557,15 +586,20 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const int oh_gstride = c->binder_tiled ? t->max_level_nodes * 8 * 64 : 64;
     const int pay_gstride = c->binder_tiled ? t->max_parents * wlw * 64 : 64;
     const int bin_rstride = c->binder_tiled ? 64 : stride;
+    // level binder buffers: the ring slots, or with the frontier cache one
+    // persistent tile per level (lc->oh / lc->pay, group stride per level)
+    auto oh_buf = [&](int lv) -> uint32_t* { return lc ? lc->oh[lv]->as<uint32_t>() : plane(wl.onehot[lv % NSLOT]); };
+    auto pay_buf = [&](int lv) -> uint32_t* { return lc ? lc->pay[lv]->as<uint32_t>() : plane(wl.payload[lv % NSLOT]); };
+    auto oh_gs = [&](int lv) -> int { return lc ? 2 * t->n_parents[lv] * 8 * 64 : oh_gstride; };
+    auto pay_gs = [&](int lv) -> int { return lc ? std::max(1, t->n_parents[lv]) * wlw * 64 : pay_gstride; };
     auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
-        const int slot = lv % NSLOT;
         AbsorbArgs ab;
-        ab.seg[0] = plane(wl.onehot[slot]);
-        ab.gstride[0] = oh_gstride;
+        ab.seg[0] = oh_buf(lv);
+        ab.gstride[0] = oh_gs(lv);
         ab.nbytes[0] = 2 * t->n_parents[lv] * 32;
         ab.f[0] = f_oh;
-        ab.seg[1] = plane(wl.payload[slot]);
-        ab.gstride[1] = pay_gstride;
+        ab.seg[1] = pay_buf(lv);
+        ab.gstride[1] = pay_gs(lv);
         ab.rstride = bin_rstride;
         ab.nbytes[1] = lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
         ab.f[1] = f_pl;
@@ -585,10 +619,28 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
         return 0;
     };
-    for (int l = 0; l <= t->L; l++) {
-        const int slot = l % NSLOT;
+    if (hit) {
+        // levels 0..L-1 from the cache: their proofs and payload differences
+        // are complete, so their sponges start right after the setup
+        hipEvent_t setup_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(setup_done, c->stream));
+        for (int lv = 0; lv < t->L; lv++) {
+            hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
+            hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
+            hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
+            HIPCHK(c, hipEventRecord(e0, c->stream));
+            HIPCHK(c, hipEventRecord(e1, c->stream));
+            HIPCHK(c, hipEventRecord(e2, c->stream));
+            HIPCHK(c, hipEventRecord(e3, c->stream));
+            if (launch_absorb(lv, setup_done, e4, e5)) return -1;
+        }
+        // the root sum of the cached level-0 evaluation (counter check)
+        HIPCHK(c, hipMemcpyAsync(pl.rootsum, lc->rootsum.p, (size_t)wlw * stride * 4, hipMemcpyDeviceToDevice,
+                                 c->stream));
+    }
+    for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
-        if (l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
+        if (!lc && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
         AesArgs a;
         a.level = l;
         a.agg_id = agg_id;
@@ -597,26 +649,28 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
-        a.cs_in = plane(wl.cs[(l + 1) & 1]);
+        a.cs_in = hit ? lc->cs[lc->wcur].as<uint32_t>() : plane(wl.cs[(l + 1) & 1]);
         a.cs_out = plane(wl.cs[l & 1]);
-        a.fr_w_in = plane(wl.fr_w[(l + 1) & 1]);
+        a.fr_w_in = hit ? lc->w[lc->wcur].as<uint32_t>() : plane(wl.fr_w[(l + 1) & 1]);
         a.fr_w_out = plane(wl.fr_w[l & 1]);
-        a.payload = plane(wl.payload[slot]);
+        a.payload = pay_buf(l);
         a.out = plane(wl.out);
         a.force_slow_blk = c->force_slow_blk;
+        a.last_w = (lc && l == t->L) ? lc->w[lc->wcur ^ 1].as<uint32_t>() : nullptr;
+        a.wp_by_node = hit ? 1 : 0;
         a.aes_waves = EVAL_WAVES - c->proof_waves;
         a.proof_prio = c->proof_prio;
         a.aes_prio = c->aes_prio;
         a.dbg_skip = c->dbg_skip;
         const int gy = (np_ + a.aes_waves * a.ppw - 1) / (a.aes_waves * a.ppw);
         a.pv_level = l - 1;
-        a.pv_nodes = l > 0 ? 2 * t->n_parents[l - 1] : 0;
+        a.pv_nodes = (l > 0 && !hit) ? 2 * t->n_parents[l - 1] : 0;  // hit: level L-1's proofs are cached
         a.pv_npw = (a.pv_nodes + gy * c->proof_waves - 1) / (gy * c->proof_waves);
         a.pv_path_bytes = (l + 7) / 8;
         a.pv_child_path = l > 0 ? t->d_path.as<uint32_t>() + t->off[l - 1] * 8 : nullptr;
-        a.pv_onehot = l > 0 ? plane(wl.onehot[(l - 1) % NSLOT]) : nullptr;
-        a.oh_gstride = oh_gstride;
-        a.pay_gstride = pay_gstride;
+        a.pv_onehot = l > 0 ? oh_buf(l - 1) : nullptr;
+        a.oh_gstride = l > 0 ? oh_gs(l - 1) : oh_gstride;
+        a.pay_gstride = pay_gs(l);
         a.bin_rstride = bin_rstride;
         a.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         a.np_f = c->pfx_f[PFX_NODE];
@@ -632,7 +686,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipEventRecord(e3, c->stream));
         hipEvent_t aes_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(aes_done, c->stream));
-        if (l > 0) {
+        if (l > 0 && !hit) {
             if (launch_absorb(l - 1, aes_done, e4, e5)) return -1;
         } else {
             HIPCHK(c, hipEventRecord(e4, c->stream2));
@@ -650,8 +704,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         pa.path_bytes = (l + 1 + 7) / 8;
         pa.child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
         pa.cs = plane(wl.cs[l & 1]);
-        pa.onehot = plane(wl.onehot[l % NSLOT]);
-        pa.oh_gstride = oh_gstride;
+        pa.onehot = oh_buf(l);
+        pa.oh_gstride = oh_gs(l);
         pa.bin_rstride = bin_rstride;
         pa.np = (const PrefixState*)c->pfx.p + PFX_NODE;
         pa.f = c->pfx_f[PFX_NODE];
@@ -679,6 +733,16 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                            flp_consts<F>(p));
     }
     HIPCHK(c, hipGetLastError());
+    if (lc) {
+        // frontier cache for the next level: last level's seeds/ctrl and payloads, root sum
+        const size_t nl = (size_t)2 * t->n_parents[t->L];
+        HIPCHK(c, hipMemcpyAsync(lc->cs[lc->wcur ^ 1].p, plane(wl.cs[t->L & 1]), nl * 5 * stride * 4,
+                                 hipMemcpyDeviceToDevice, c->stream));
+        if (!hit)
+            HIPCHK(c, hipMemcpyAsync(lc->rootsum.p, pl.rootsum, (size_t)wlw * stride * 4, hipMemcpyDeviceToDevice,
+                                     c->stream));
+        lc->wcur ^= 1;
+    }
     // results -> the agg_id slot (plane stride = all reports)
     Result& R = c->res[agg_id];
     int rc = 0;
@@ -752,16 +816,71 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
     if (!c->work.ensure(per_report * (chunk + pad)))
         return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * (chunk + pad));
+    // frontier cache (one-chunk batches with tiled binder buffers only)
+    LevelCache* lc = nullptr;
+    bool hit = false;
+    std::vector<uint8_t> lkey(verify_key, verify_key + 32);
+    lkey.insert(lkey.end(), app_ctx, app_ctx + ctx_len);
+    if (c->frontier_cache && c->binder_tiled && chunk >= n) {
+        lc = &c->lc[agg_id];
+        const int stride1 = (int)(round_up(n, 64) + pad);
+        const int L = t->L;
+        hit = lc->valid && lc->rep_gen == rep->gen && lc->n == n && lc->stride == stride1 && lc->key == lkey &&
+              !t->weight_check && L == lc->L + 1 && (size_t)L <= lc->n_parents.size() &&
+              std::equal(t->n_parents.begin(), t->n_parents.begin() + L, lc->n_parents.begin()) &&
+              lc->paths.size() == t->off[L] * 8 &&
+              std::equal(lc->paths.begin(), lc->paths.end(), t->child_path.begin());
+        // tiles for every 64-row group of the padded stride: the sponge
+        // kernels run over all pl.stride rows, padding included
+        const size_t S1 = (size_t)stride1, groups = S1 / 64;
+        const size_t wlw = (size_t)p.value_len * p.w32;
+        bool ok = true;
+        if ((int)lc->oh.size() < L + 1) {
+            lc->oh.resize(L + 1);
+            lc->pay.resize(L + 1);
+        }
+        for (int lv = 0; lv <= L && ok; lv++) {
+            if (!lc->oh[lv]) lc->oh[lv].reset(new DevBuf());
+            if (!lc->pay[lv]) lc->pay[lv].reset(new DevBuf());
+            if (hit && lv < L) continue;  // cached
+            ok = lc->oh[lv]->ensure(groups * 2 * t->n_parents[lv] * 8 * 64 * 4) &&
+                 lc->pay[lv]->ensure(groups * std::max(1, t->n_parents[lv]) * wlw * 64 * 4);
+        }
+        const size_t nl = (size_t)2 * t->n_parents[L];
+        ok = ok && lc->cs[lc->wcur ^ 1].ensure(nl * 5 * S1 * 4) && lc->w[lc->wcur ^ 1].ensure(nl * wlw * S1 * 4) &&
+             lc->rootsum.ensure(wlw * S1 * 4);
+        if (!ok) {  // not enough HBM for the cache: evaluate without it
+            lc->drop();
+            lc = nullptr;
+            hit = false;
+        }
+    } else {
+        c->lc[agg_id].drop();
+    }
     size_t evi = 0;
     hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
     HIPCHK(c, hipEventRecord(t0, c->stream));
     for (size_t b = 0; b < n; b += chunk) {
         const int nn = (int)std::min(chunk, n - b);
         const int stride = (int)(round_up(nn, 64) + pad);
-        rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi)
-                           : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi);
-        if (rc) return rc;
+        rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit)
+                           : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit);
+        if (rc) {
+            if (lc) lc->drop();
+            return rc;
+        }
     }
+    if (lc) {
+        lc->valid = true;
+        lc->rep_gen = rep->gen;
+        lc->n = n;
+        lc->stride = (int)(round_up(n, 64) + pad);
+        lc->key = lkey;
+        lc->L = t->L;
+        lc->n_parents.assign(t->n_parents.begin(), t->n_parents.begin() + t->L + 1);
+        lc->paths.assign(t->child_path.begin(), t->child_path.begin() + (t->off[t->L] + 2 * t->n_parents[t->L]) * 8);
+    }
+    c->last_hit = hit;
     HIPCHK(c, hipEventRecord(t1, c->stream));
     c->n_eval = -(int)evi;  // timing pending (resolved by mastic_last_timing)
     R.ready = true;
@@ -1073,6 +1192,7 @@ extern "C" int mastic_reports_upload(mastic_reports* r, const uint8_t* nonces, c
     mastic_ctx* c = r->ctx;
     const McParams& p = c->p;
     const size_t n = r->n;
+    r->gen = ++g_reports_gen;
     if (nonces) HIPCHK(c, hipMemcpy(r->nonces.p, nonces, 16 * n, hipMemcpyHostToDevice));
     if (pub) HIPCHK(c, hipMemcpy(r->pub.p, pub, (size_t)mc_public_share_size(p) * n, hipMemcpyHostToDevice));
     if (in0) {
@@ -1183,6 +1303,7 @@ extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx,
     DeviceScope ds_(rep ? rep->ctx : nullptr);
     if (!rep) return MASTIC_EINVAL;
     mastic_ctx* c = rep->ctx;
+    rep->gen = ++g_reports_gen;
     if (rep->n == 0) return 0;
     if (!alphas || !nonces || !rands || (!betas && c->p.meas_len > 0)) return fail(c, MASTIC_EINVAL, "null input");
     int rc = build_prefixes(c, app_ctx, ctx_len, nullptr);
@@ -1284,6 +1405,26 @@ extern "C" void mastic_ctx_destroy(mastic_ctx* c) {
 }
 
 extern "C" const char* mastic_last_error(const mastic_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
+    if (!c) return MASTIC_EINVAL;
+    if (on >= 0) {
+        c->frontier_cache = on != 0;
+        if (!on)
+            for (auto& x : c->lc) {
+                x.drop();
+                x.oh.clear();
+                x.pay.clear();
+                x.cs[0].release();
+                x.cs[1].release();
+                x.w[0].release();
+                x.w[1].release();
+                x.rootsum.release();
+            }
+    }
+    if (last_hit) *last_hit = c->last_hit ? 1 : 0;
+    return 0;
+}
 
 extern "C" int mastic_set_memory_budget(mastic_ctx* c, uint64_t bytes) {
     if (!c) return MASTIC_EINVAL;

@@ -29,7 +29,7 @@ EXPORTS = [
     "mastic_reports_shard", "mastic_prep_init", "mastic_prep_result", "mastic_aggregate",
     "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
     "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
-    "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree",
+    "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
 ]
 
 
@@ -122,6 +122,7 @@ def lib():
                                             + [ctypes.POINTER(ctypes.c_double)]),
                     "mastic_work_bytes": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64)]),
                     "mastic_proof_tree": (i32, [P, ctypes.c_int, u8p, sz, P, sz]),
+                    "mastic_set_frontier_cache": (i32, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
                     "mastic_tree_stats": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64),
                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
                 }

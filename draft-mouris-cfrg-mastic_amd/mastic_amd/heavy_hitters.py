@@ -55,7 +55,7 @@ class SweepLevel:
 
 
 def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verify_key: bytes = None,
-                          trace=None, merge=None, timing=None):
+                          trace=None, merge=None, timing=None, frontier_cache=None, cached_levels=None):
     """poc/examples.py:37-91 on the GPU.
 
     ``reports`` is either the reference's list of
@@ -67,7 +67,13 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     rank's agg share (list of field elements) to the job-wide one (all
     ranks call it at every level, in the same order).  If ``timing`` is a
     list, ``mastic.last_timing3()`` of every prep_init is appended to it.
+    ``frontier_cache`` (True/False) switches the GPU frontier cache
+    (``Mastic.set_frontier_cache``): each level then evaluates only its new
+    tree level when the previous level's tree is unchanged; if
+    ``cached_levels`` is a list, the levels that took that path are appended.
     """
+    if frontier_cache is not None:
+        mastic.set_frontier_cache(frontier_cache)
     if verify_key is None:
         import os
         verify_key = os.urandom(mastic.VERIFY_KEY_SIZE)
@@ -97,6 +103,8 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                 shares.append(mastic.prep_result(dev, agg_id, enc))
                 if timing is not None:
                     timing.append(mastic.last_timing3())
+                if cached_levels is not None and agg_id == 0 and frontier_cache and mastic.last_prep_was_cached():
+                    cached_levels.append(level)
             (_msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
             alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
             mask = alive.astype(np.uint8)

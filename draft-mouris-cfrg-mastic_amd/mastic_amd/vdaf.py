@@ -297,6 +297,17 @@ class Mastic:
                                                        ctypes.byref(b), ctypes.byref(c)))
         return (a.value, b.value, c.value)
 
+    def set_frontier_cache(self, on: bool):
+        """Keep each prep_init's per-level binder inputs and last frontier in HBM so
+        that the next level of a sweep evaluates only its new level (C ABI
+        mastic_set_frontier_cache); results are identical either way."""
+        _check(self._ctx, _lib.lib().mastic_set_frontier_cache(self._ctx, 1 if on else 0, None))
+
+    def last_prep_was_cached(self) -> bool:
+        v = ctypes.c_int()
+        _check(self._ctx, _lib.lib().mastic_set_frontier_cache(self._ctx, -1, ctypes.byref(v)))
+        return bool(v.value)
+
     def proof_tree(self, agg_id: int, ctx: bytes, n: int):
         """Merkle tree over the eval proofs of the last prep_init of agg_id
         over n reports (proof-aggregation mode, see mastic_amd.proof_agg):

@@ -141,6 +141,17 @@ int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares,
  * every report's eval proofs agree (mastic.py:340). */
 int mastic_proof_tree(mastic_ctx* ctx, int agg_id, const uint8_t* app_ctx, size_t ctx_len, uint8_t* nodes_out,
                       size_t n_nodes);
+/* Frontier cache for level sweeps (the reference's
+ * examples.py:37-91 re-evaluates the whole tree at every level).  on = 1
+ * enables it, 0 disables it and frees its buffers, -1 leaves it unchanged.
+ * With it on, prep_init keeps per report every level's node proofs and payload
+ * differences plus the last level's seeds and payloads (HBM: ~48 B per node
+ * per report and aggregator); a later prep_init for the same reports, agg_id,
+ * verify key and ctx whose tree is the cached tree plus one level (the sweep
+ * with no candidate path pruned away) evaluates only that level and re-absorbs
+ * the rest from the cache.  Results are identical either way.  *last_hit (if
+ * not NULL) = 1 when the last prep_init took the cached path. */
+int mastic_set_frontier_cache(mastic_ctx* ctx, int on, int* last_hit);
 /* Wait for all enqueued work of the ctx. */
 int mastic_synchronize(mastic_ctx* ctx);
 

@@ -1,0 +1,103 @@
+"""Frontier cache for level sweeps (Mastic.set_frontier_cache).
+
+With the cache on, a prep_init whose tree is the previous call's tree plus one
+level evaluates only that level and re-absorbs the cached proofs and payload
+differences.  The results must be bit-identical to a full evaluation: checked
+level by level against a second context with the cache off, against the CPU
+oracle for sampled reports, and end to end through the sweep driver."""
+import random
+
+import pytest
+
+from test_gpu_parity import CTX, _oracle_for, mastic_amd  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _reports(m, rng, n, pool_size):
+    pool = [tuple(bool(rng.getrandbits(1)) for _ in range(m.BITS)) for _ in range(pool_size)]
+    alphas = [pool[min(int(rng.paretovariate(1.0)) - 1, pool_size - 1)] for _ in range(n)]
+    weights = [rng.randrange(2) for _ in range(n)] if m.circuit == "Count" else \
+        [rng.randrange(m.max_measurement + 1) for _ in range(n)]
+    nonces = bytes(rng.getrandbits(8) for _ in range(16 * n))
+    rands = bytes(rng.getrandbits(8) for _ in range(m.RAND_SIZE * n))
+    return alphas, weights, nonces, rands
+
+
+@pytest.mark.parametrize("circuit,kw", [("Count", dict(bits=10)), ("Sum", dict(bits=9, max_measurement=5))],
+                         ids=["Count", "Sum"])
+def test_cached_levels_bit_identical(mastic_amd, circuit, kw):
+    from mastic_amd.heavy_hitters import compute_heavy_hitters
+    rng = random.Random(77)
+    kw = dict(kw)
+    bits = kw.pop("bits")
+    m_off = mastic_amd.Mastic(bits, circuit, **kw)
+    m_on = mastic_amd.Mastic(bits, circuit, **kw)
+    o = _oracle_for(m_off)
+    n = 150
+    (alphas, weights, nonces, rands) = _reports(m_off, rng, n, 12)
+    (pub, in0, in1) = m_off.shard_batch(CTX, alphas, weights, nonces, rands)
+    vk = bytes(rng.getrandbits(8) for _ in range(32))
+    # the per-level candidate lists of a real sweep (cache off)
+    trace = []
+    dev_off = m_off.reports_upload(nonces, pub, in0, in1)
+    hh = compute_heavy_hitters(m_off, CTX, {"default": 4}, dev_off, verify_key=vk, trace=trace)
+    assert trace[-1].prefixes, "the workload should keep candidates down to the last level"
+    dev_on = m_on.reports_upload(nonces, pub, in0, in1)
+    m_on.set_frontier_cache(True)
+    hits = 0
+    psz, isz = m_off.public_share_size(), m_off.input_share_size(1)
+    for lv in trace:
+        if not lv.prefixes:
+            break
+        ap = (lv.level, tuple(lv.prefixes), lv.level == 0)
+        for agg_id in range(2):
+            m_off.prep_init_device(dev_off, vk, CTX, agg_id, ap)
+            m_on.prep_init_device(dev_on, vk, CTX, agg_id, ap)
+            a = m_off.prep_result(dev_off, agg_id, ap, want_out_shares=True)
+            b = m_on.prep_result(dev_on, agg_id, ap, want_out_shares=True)
+            assert a[0] == b[0] and a[2] == b[2], "level %d agg %d" % (lv.level, agg_id)
+            if m_on.last_prep_was_cached():
+                hits += 1
+                if agg_id == 1 and hits <= 8:
+                    # sampled reports of a cached level through the oracle
+                    for i in (0, n - 1):
+                        cws = o.vidpf.decode_public_share(pub[psz * i:psz * (i + 1)])
+                        isd = o.decode_input_share(1, in1[isz * i:isz * (i + 1)])
+                        (_st, sh) = o.prep_init(vk, CTX, 1, ap, nonces[16 * i:16 * (i + 1)], cws, isd)
+                        enc = o.test_vec_encode_prep_share(sh)
+                        assert b[0][len(enc) * i:len(enc) * (i + 1)] == enc
+    assert hits >= 2, hits  # levels whose tree extends the previous one take the cached path
+    # the sweep driver with the cache gives the same heavy hitters
+    cached = []
+    assert compute_heavy_hitters(m_on, CTX, {"default": 4}, dev_on, verify_key=vk, frontier_cache=True,
+                                 cached_levels=cached) == hh
+    assert len(cached) >= 1
+    m_on.set_frontier_cache(False)
+
+
+def test_cache_not_used_across_different_inputs(mastic_amd):
+    """A cached tree is only reused for the same reports, agg_id, verify key
+    and ctx: changing any of them evaluates the whole tree."""
+    rng = random.Random(78)
+    m = mastic_amd.MasticCount(6)
+    (alphas, weights, nonces, rands) = _reports(m, rng, 70, 4)
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    dev = m.reports_upload(nonces, pub, in0, in1)
+    m.set_frontier_cache(True)
+    vk = bytes(32)
+    p0 = tuple(sorted(set(a[:1] for a in alphas)))
+    p1 = tuple(sorted(set(a[:2] for a in alphas) | set(p + (b,) for p in p0 for b in (False, True))))
+    m.prep_init_device(dev, vk, CTX, 0, (0, ((False,), (True,)), False))
+    m.prep_init_device(dev, vk, CTX, 0, (1, p1, False))
+    assert m.last_prep_was_cached()
+    m.prep_init_device(dev, vk, CTX, 0, (0, ((False,), (True,)), False))
+    m.prep_init_device(dev, bytes([1]) * 32, CTX, 0, (1, p1, False))  # other verify key
+    assert not m.last_prep_was_cached()
+    m.prep_init_device(dev, vk, CTX, 0, (0, ((False,), (True,)), False))
+    m.prep_init_device(dev, vk, CTX + b"x", 0, (1, p1, False))  # other ctx
+    assert not m.last_prep_was_cached()
+    m.prep_init_device(dev, vk, CTX, 0, (0, ((False,), (True,)), False))
+    m.prep_init_device(dev, vk, CTX, 1, (1, p1, False))  # other aggregator
+    assert not m.last_prep_was_cached()
+    m.set_frontier_cache(False)
