@@ -533,8 +533,11 @@ struct AesArgs {
 #define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(EVAL_MIN_WAVES)))
 #define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16 + 16)
 // QUAD: payload refills of 2 blocks per sibling (4-block lockstep AES) instead
-// of 1 (paired); chosen at run time (mastic_ctx::eval_quad).
-template <class F, bool QUAD>
+// of 1 (paired); chosen at run time (mastic_ctx::eval_quad).  FC: the frontier
+// cache's last-level payload stores and parent indirection (AesArgs::last_w,
+// wp_by_node) are compiled in; the plain instantiation carries none of it
+// (the uniform branches cost 2.5 % at C2).
+template <class F, bool QUAD, bool FC>
 __global__ __launch_bounds__(64 * EVAL_WAVES) EVAL_VGPR_ATTR
 void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
@@ -690,9 +693,11 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             if (tc1) x1 = F::add(x1, cw);
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
-            if (a.last_w) {
-                pl_store<F>(a.last_w, (2 * pi) * vl + e, S, r, x0);
-                pl_store<F>(a.last_w, (2 * pi + 1) * vl + e, S, r, x1);
+            if constexpr (FC) {
+                if (a.last_w) {
+                    pl_store<F>(a.last_w, (2 * pi) * vl + e, S, r, x0);
+                    pl_store<F>(a.last_w, (2 * pi + 1) * vl + e, S, r, x1);
+                }
             }
             if (l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
@@ -729,7 +734,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             }
         };
         auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
-        const int wpi = a.wp_by_node ? a.parent_node[pi] : pi;
+        int wpi = pi;
+        if constexpr (FC) wpi = a.wp_by_node ? a.parent_node[pi] : pi;
         auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, wpi * vl + e, S, r) : F::zero(); };
         int e_fast = 0;  // elements completed by the fast path
         if constexpr (!QUAD) {

@@ -679,7 +679,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
         hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        hipLaunchKernelGGL((k_eval_aes<F, false>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream, p, pl, a);
+        if (lc)
+            hipLaunchKernelGGL((k_eval_aes<F, false, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
+                               p, pl, a);
+        else
+            hipLaunchKernelGGL((k_eval_aes<F, false, false>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
+                               p, pl, a);
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(e2, c->stream));
@@ -1372,9 +1377,13 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     }
     // the level kernel's LDS (table + key schedules) is dynamic, above the
     // 64 KiB default
-    if (hipFuncSetAttribute((const void*)k_eval_aes<F64, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)k_eval_aes<F64, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_eval_aes<F128, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F64, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_absorb_pair, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess) {
