@@ -50,7 +50,7 @@ CONFIGS = {
                     desc="C1: Mastic(BITS=16, Count) weighted heavy hitters, full 16-level sweep (Zipf(1.2) over "
                          "128 random 16-bit strings, weights Bernoulli(0.9), threshold 10), both aggregators per "
                          "level: the reference's CPU-sized case"),
-    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=16384, sweep=True, pool=2 ** 20, zipf=1.1,
+    "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=65536, sweep=True, pool=2 ** 20, zipf=1.1,
                     weight_p=1.0, threshold=None,
                     desc="C3: Mastic(BITS=256, Count) weighted heavy hitters, full 256-level threshold-pruned "
                          "sweep (Zipf(1.1) over 2^20 random 256-bit strings, threshold 0.05% of all reports), "

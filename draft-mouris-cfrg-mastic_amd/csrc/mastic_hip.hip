@@ -71,11 +71,11 @@ inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 // Frontier cache of one aggregator (mastic_set_frontier_cache; SURVEY.md §8f
 // row 1).  In a level sweep (examples.py:37-91) prep_init at level L evaluates
 // the whole tree again, but its levels 0..L-1 are usually exactly the previous
-// call's tree.  The cache keeps, per report, every level's node proofs and
-// payload differences (the binder inputs, tiled as in the ring buffers), the
-// last level's child seeds / control bits and payloads, and the root sum;
-// a call whose tree extends the cached one by one level evaluates only that
-// level and re-absorbs the rest from the cache.
+// call's tree.  The cache keeps, per report, the two binder sponges' states
+// after the cached call's levels (the binder messages are BFS-ordered, so the
+// cached message is a prefix of the next one), the last level's child seeds /
+// control bits and payloads, and the root sum; a call whose tree extends the
+// cached one by one level evaluates and absorbs only that level.
 struct LevelCache {
     bool valid = false;
     uint64_t rep_gen = 0;
@@ -85,7 +85,7 @@ struct LevelCache {
     int L = -1;                                 // level of the cached call
     std::vector<int> n_parents;                 // per level 0..L
     std::vector<uint32_t> paths;                // child paths of levels 0..L (8 words per node)
-    std::vector<std::unique_ptr<DevBuf>> oh, pay;  // per level: proofs tile, payload-difference tile
+    DevBuf sp;                                  // both binder sponges after levels 0..L (2 x 50 planes)
     DevBuf cs[2], w[2], rootsum;                // last level's seeds/ctrl and payloads; root sum
     int wcur = 0;                               // which cs / w hold the cached level (the other is written)
     void drop() { valid = false; }
@@ -586,12 +586,13 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const int oh_gstride = c->binder_tiled ? t->max_level_nodes * 8 * 64 : 64;
     const int pay_gstride = c->binder_tiled ? t->max_parents * wlw * 64 : 64;
     const int bin_rstride = c->binder_tiled ? 64 : stride;
-    // level binder buffers: the ring slots, or with the frontier cache one
-    // persistent tile per level (lc->oh / lc->pay, group stride per level)
-    auto oh_buf = [&](int lv) -> uint32_t* { return lc ? lc->oh[lv]->as<uint32_t>() : plane(wl.onehot[lv % NSLOT]); };
-    auto pay_buf = [&](int lv) -> uint32_t* { return lc ? lc->pay[lv]->as<uint32_t>() : plane(wl.payload[lv % NSLOT]); };
-    auto oh_gs = [&](int lv) -> int { return lc ? 2 * t->n_parents[lv] * 8 * 64 : oh_gstride; };
-    auto pay_gs = [&](int lv) -> int { return lc ? std::max(1, t->n_parents[lv]) * wlw * 64 : pay_gstride; };
+    // level binder buffers: the ring slots (with the frontier cache too: a
+    // hit resumes both sponges from their cached states, so no level's
+    // proofs or payload differences outlive the call)
+    auto oh_buf = [&](int lv) -> uint32_t* { return plane(wl.onehot[lv % NSLOT]); };
+    auto pay_buf = [&](int lv) -> uint32_t* { return plane(wl.payload[lv % NSLOT]); };
+    auto oh_gs = [&](int) -> int { return oh_gstride; };
+    auto pay_gs = [&](int) -> int { return pay_gstride; };
     auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
         AbsorbArgs ab;
         ab.seg[0] = oh_buf(lv);
@@ -620,10 +621,14 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         return 0;
     };
     if (hit) {
-        // levels 0..L-1 from the cache: their proofs and payload differences
-        // are complete, so their sponges start right after the setup
-        hipEvent_t setup_done = get_sync_event(c, sev++);
-        HIPCHK(c, hipEventRecord(setup_done, c->stream));
+        // levels 0..L-1 from the cache.  The binder messages are BFS-ordered
+        // (mastic.py:263-275), so the cached call's message is a prefix of
+        // this one's: both sponges resume from their states at the end of the
+        // cached call (mid-block, unpadded; k_finalize pads a register copy).
+        HIPCHK(c, hipMemcpyAsync(pl.sp_onehot, lc->sp.p, (size_t)50 * stride * 4, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        HIPCHK(c, hipMemcpyAsync(pl.sp_payload, lc->sp.as<uint32_t>() + (size_t)50 * stride,
+                                 (size_t)50 * stride * 4, hipMemcpyDeviceToDevice, c->stream));
         for (int lv = 0; lv < t->L; lv++) {
             hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
             hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
@@ -632,7 +637,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             HIPCHK(c, hipEventRecord(e1, c->stream));
             HIPCHK(c, hipEventRecord(e2, c->stream));
             HIPCHK(c, hipEventRecord(e3, c->stream));
-            if (launch_absorb(lv, setup_done, e4, e5)) return -1;
+            HIPCHK(c, hipEventRecord(e4, c->stream));
+            HIPCHK(c, hipEventRecord(e5, c->stream));
+            f_oh = (f_oh + 2 * t->n_parents[lv] * 32) % KECCAK_RATE;
+            f_pl = (f_pl + (lv > 0 ? t->n_parents[lv] * wlw * 4 : 0)) % KECCAK_RATE;
         }
         // the root sum of the cached level-0 evaluation (counter check)
         HIPCHK(c, hipMemcpyAsync(pl.rootsum, lc->rootsum.p, (size_t)wlw * stride * 4, hipMemcpyDeviceToDevice,
@@ -640,7 +648,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     }
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
-        if (!lc && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
+        if (!hit && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
         AesArgs a;
         a.level = l;
         a.agg_id = agg_id;
@@ -746,6 +754,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         if (!hit)
             HIPCHK(c, hipMemcpyAsync(lc->rootsum.p, pl.rootsum, (size_t)wlw * stride * 4, hipMemcpyDeviceToDevice,
                                      c->stream));
+        // both sponges after levels 0..L (stream waited for abs_done[L] above)
+        HIPCHK(c, hipMemcpyAsync(lc->sp.p, pl.sp_onehot, (size_t)50 * stride * 4, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        HIPCHK(c, hipMemcpyAsync(lc->sp.as<uint32_t>() + (size_t)50 * stride, pl.sp_payload,
+                                 (size_t)50 * stride * 4, hipMemcpyDeviceToDevice, c->stream));
         lc->wcur ^= 1;
     }
     // results -> the agg_id slot (plane stride = all reports)
@@ -839,21 +852,10 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         // kernels run over all pl.stride rows, padding included
         const size_t S1 = (size_t)stride1, groups = S1 / 64;
         const size_t wlw = (size_t)p.value_len * p.w32;
-        bool ok = true;
-        if ((int)lc->oh.size() < L + 1) {
-            lc->oh.resize(L + 1);
-            lc->pay.resize(L + 1);
-        }
-        for (int lv = 0; lv <= L && ok; lv++) {
-            if (!lc->oh[lv]) lc->oh[lv].reset(new DevBuf());
-            if (!lc->pay[lv]) lc->pay[lv].reset(new DevBuf());
-            if (hit && lv < L) continue;  // cached
-            ok = lc->oh[lv]->ensure(groups * 2 * t->n_parents[lv] * 8 * 64 * 4) &&
-                 lc->pay[lv]->ensure(groups * std::max(1, t->n_parents[lv]) * wlw * 64 * 4);
-        }
+        (void)groups;
         const size_t nl = (size_t)2 * t->n_parents[L];
-        ok = ok && lc->cs[lc->wcur ^ 1].ensure(nl * 5 * S1 * 4) && lc->w[lc->wcur ^ 1].ensure(nl * wlw * S1 * 4) &&
-             lc->rootsum.ensure(wlw * S1 * 4);
+        const bool ok = lc->sp.ensure(100 * S1 * 4) && lc->cs[lc->wcur ^ 1].ensure(nl * 5 * S1 * 4) &&
+                        lc->w[lc->wcur ^ 1].ensure(nl * wlw * S1 * 4) && lc->rootsum.ensure(wlw * S1 * 4);
         if (!ok) {  // not enough HBM for the cache: evaluate without it
             lc->drop();
             lc = nullptr;
@@ -1422,8 +1424,7 @@ extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
         if (!on)
             for (auto& x : c->lc) {
                 x.drop();
-                x.oh.clear();
-                x.pay.clear();
+                x.sp.release();
                 x.cs[0].release();
                 x.cs[1].release();
                 x.w[0].release();

@@ -1,8 +1,8 @@
 """Frontier cache for level sweeps (Mastic.set_frontier_cache).
 
 With the cache on, a prep_init whose tree is the previous call's tree plus one
-level evaluates only that level and re-absorbs the cached proofs and payload
-differences.  The results must be bit-identical to a full evaluation: checked
+level evaluates only that level and resumes both binder sponges from their
+cached states.  The results must be bit-identical to a full evaluation: checked
 level by level against a second context with the cache off, against the CPU
 oracle for sampled reports, and end to end through the sweep driver."""
 import random
