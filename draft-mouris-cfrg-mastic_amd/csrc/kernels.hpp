@@ -106,7 +106,9 @@ struct Planes {
 // (poc/vidpf.py:382-394).  Input share: key || [leader proof share] || [seed]
 // || [peer jr part] (poc/mastic.py:516-529).
 __global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_id, const uint8_t* nonces,
-                                                const uint8_t* pub, const uint8_t* ins) {
+                                                const uint8_t* pub, const uint8_t* ins, int l_lo, int l_hi) {
+    // correction words of levels l_lo .. l_hi-1 only: a call at level L never
+    // reads deeper ones, and a frontier-cache hit only reads level L's
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= pl.n) return;
     const int S = pl.stride;
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_i
         pl.nonce[i * S + r] = ld_u32_bytes(nc + 4 * i);
         pl.key[i * S + r] = ld_u32_bytes(is + 4 * i);
     }
-    for (int l = 0; l < p.bits; l++) {
+    for (int l = l_lo; l < l_hi; l++) {
         uint32_t c0 = (ps[(2 * l) >> 3] >> ((2 * l) & 7)) & 1;
         uint32_t c1 = (ps[(2 * l + 1) >> 3] >> ((2 * l + 1) & 7)) & 1;
         pl.cw_ctrl[(size_t)l * S + r] = c0 | (c1 << 1);

@@ -130,6 +130,7 @@ struct mastic_ctx {
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
+    std::vector<uint8_t> pfx_key;  // verify key || ctx of the prefix states in pfx (empty: none)
     std::map<std::vector<uint8_t>, Tree*> trees;
     Result res[2];
     bool frontier_cache = false;  // mastic_set_frontier_cache
@@ -206,6 +207,11 @@ static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len,
     static const uint8_t zero_vk[32] = {0};
     if (!vk) vk = zero_vk;
     if (ctx_len > 65535 - 12) return fail(c, MASTIC_EINVAL, "ctx too long");
+    std::vector<uint8_t> key(vk, vk + 32);
+    key.insert(key.end(), app_ctx, app_ctx + ctx_len);
+    key.push_back(1);  // never equal to the empty "none" key
+    if (key == c->pfx_key) return 0;  // same verify key and ctx as the states already in pfx
+    c->pfx_key.clear();
     std::vector<std::vector<uint8_t>> m(PFX_COUNT);
     auto xof_ts = [&](int id, const std::vector<uint8_t>& d, int seed_len, const uint8_t* seed) {
         put_le16(m[id], (uint32_t)d.size());
@@ -251,6 +257,7 @@ static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len,
     HIPCHK(c, hipMemcpyAsync(c->pfx_host, c->pfx.p, sizeof(PrefixState) * PFX_COUNT, hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->pfx_key = std::move(key);
     return 0;
 }
 
@@ -306,12 +313,10 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         if (tail_bits && (pfx[i][plen - 1] & ((1u << (8 - tail_bits)) - 1)))
             return fail(c, MASTIC_EINVAL, "prefix with incorrect length");
     }
-    {
-        std::vector<std::vector<uint8_t>> s = pfx;
-        std::sort(s.begin(), s.end());
-        if (std::adjacent_find(s.begin(), s.end()) != s.end())
-            return fail(c, MASTIC_EINVAL, "candidate prefixes are non-unique");
-    }
+    std::vector<std::vector<uint8_t>> sorted_pfx = pfx;
+    std::sort(sorted_pfx.begin(), sorted_pfx.end());
+    if (std::adjacent_find(sorted_pfx.begin(), sorted_pfx.end()) != sorted_pfx.end())
+        return fail(c, MASTIC_EINVAL, "candidate prefixes are non-unique");
     std::map<std::vector<uint8_t>, int> pfx_index;
     for (uint64_t i = 0; i < count; i++) pfx_index[pfx[i]] = (int)i;
 
@@ -330,8 +335,9 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
     for (int l = 0; l < level; l++) {
         std::vector<std::vector<uint8_t>> v;
         v.reserve(count);
-        for (auto& q : pfx) v.push_back(truncate(q, l + 1));
-        std::sort(v.begin(), v.end());
+        // truncation keeps the MSB-first byte order, so the truncated sorted
+        // list is sorted already (no per-level sort: 255 of them per C3 tree)
+        for (auto& q : sorted_pfx) v.push_back(truncate(q, l + 1));
         v.erase(std::unique(v.begin(), v.end()), v.end());
         exp[l] = std::move(v);
     }
@@ -561,7 +567,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const uint8_t* ins = agg_id == 0 ? rep->in0.as<uint8_t>() : rep->in1.as<uint8_t>();
     const PrefixState* pfx = (const PrefixState*)c->pfx.p;
     hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
-                       rep->nonces.as<uint8_t>() + 16 * base, rep->pub.as<uint8_t>() + ps * base, ins + is * base);
+                       rep->nonces.as<uint8_t>() + 16 * base, rep->pub.as<uint8_t>() + ps * base, ins + is * base,
+                       hit ? t->L : 0, t->L + 1);
     hipLaunchKernelGGL(k_setup, dim3((stride + 255) / 256), dim3(256), 0, c->stream, pl, pfx);
     HIPCHK(c, hipGetLastError());
 
@@ -629,16 +636,9 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                                  c->stream));
         HIPCHK(c, hipMemcpyAsync(pl.sp_payload, lc->sp.as<uint32_t>() + (size_t)50 * stride,
                                  (size_t)50 * stride * 4, hipMemcpyDeviceToDevice, c->stream));
+        // (no timing events for the cached levels: nothing is launched for
+        // them, and 6 records per level cost ~1.4 ms of host time at L = 255)
         for (int lv = 0; lv < t->L; lv++) {
-            hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
-            hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
-            hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
-            HIPCHK(c, hipEventRecord(e0, c->stream));
-            HIPCHK(c, hipEventRecord(e1, c->stream));
-            HIPCHK(c, hipEventRecord(e2, c->stream));
-            HIPCHK(c, hipEventRecord(e3, c->stream));
-            HIPCHK(c, hipEventRecord(e4, c->stream));
-            HIPCHK(c, hipEventRecord(e5, c->stream));
             f_oh = (f_oh + 2 * t->n_parents[lv] * 32) % KECCAK_RATE;
             f_pl = (f_pl + (lv > 0 ? t->n_parents[lv] * wlw * 4 : 0)) % KECCAK_RATE;
         }

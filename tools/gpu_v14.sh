@@ -1,0 +1,5 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/prof_v14
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_v14/c3sweep -o run --output-format csv -- python3 bench.py --config c3sweep --steps 1 --warmup 0 --cpu-baseline 0 > gpurun_out/prof_v14/c3sweep_stats.log 2>&1 && \
+timeout -k 10 400 python3 -m cProfile -s cumtime bench.py --config c3sweep --steps 1 --warmup 0 --cpu-baseline 0 > gpurun_out/prof_v14/c3sweep_cprofile.txt 2>&1
