@@ -97,14 +97,18 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
         enc = mastic.encode_agg_param(agg_param)  # once per level: the batch calls take the encoding
 
         if n and prefixes:
-            shares = []
+            # both aggregators' prep_init are queued before either result is
+            # fetched, so the host work of the second overlaps the GPU run of
+            # the first (stream-ordered; results and timings are per agg_id)
             for agg_id in range(2):
                 mastic.prep_init_device(dev, verify_key, ctx, agg_id, enc)
+                if cached_levels is not None and agg_id == 0 and frontier_cache and mastic.last_prep_was_cached():
+                    cached_levels.append(level)
+            shares = []
+            for agg_id in range(2):
                 shares.append(mastic.prep_result(dev, agg_id, enc))
                 if timing is not None:
                     timing.append(mastic.last_timing3())
-                if cached_levels is not None and agg_id == 0 and frontier_cache and mastic.last_prep_was_cached():
-                    cached_levels.append(level)
             (_msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
             alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
             mask = alive.astype(np.uint8)
