@@ -44,6 +44,35 @@ def _encode_reports(mastic: Mastic, reports):
     return (nonces, pubs, in0, in1)
 
 
+def _child_packed(packed: bytes, level: int, bit: bool) -> bytes:
+    """MSB-first packing (vidpf.py:33-39) of ``prefix + (bit,)`` from the
+    packing of the length-``level`` ``prefix``."""
+    if level % 8 == 0:
+        packed += b"\x00"
+    if bit:
+        packed = packed[:-1] + bytes([packed[-1] | (0x80 >> (level % 8))])
+    return packed
+
+
+def _unshard_raw(mastic: Mastic, raw_shares, num_measurements):
+    """``mastic.unshard`` (mastic.py:399-411) on the two aggregators'
+    encode_vec agg shares, summed as integers mod p (same result, without a
+    field object per share element)."""
+    f = mastic.field
+    enc = f.ENCODED_SIZE
+    if enc == 8:
+        vecs = [np.frombuffer(r, dtype="<u8").tolist() for r in raw_shares]
+    else:
+        vecs = [[int.from_bytes(r[i:i + enc], "little") for i in range(0, len(r), enc)] for r in raw_shares]
+    p = f.MODULUS
+    for v in vecs:
+        if v and max(v) >= p:
+            raise ValueError("encoded element out of range")
+    agg = [f((a + b) % p) for (a, b) in zip(*vecs)]
+    k = 1 + mastic.OUTPUT_LEN
+    return [mastic.decode_result(agg[i + 1:i + k], agg[i].int()) for i in range(0, len(agg), k)]
+
+
 class SweepLevel:
     """What one level of the sweep did (for callers that want the trace)."""
 
@@ -88,13 +117,21 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     alive = np.ones(n, dtype=bool)
 
     prefixes = [(False,), (True,)]
+    fast = isinstance(mastic, Mastic)
+    packed = [b"\x00", b"\x80"]  # MSB-first packings of ``prefixes`` (fast path)
     prev_agg_params = []
     heavy_hitters = []
     bits = mastic.vidpf.BITS
     for level in range(bits):
         agg_param = (level, tuple(prefixes), level == 0)
         assert mastic.is_valid(agg_param, prev_agg_params)
-        enc = mastic.encode_agg_param(agg_param)  # once per level: the batch calls take the encoding
+        # encoded once per level (the batch calls take the bytes); the fast
+        # path extends the parents' packings instead of re-packing every bit
+        if fast:
+            enc = (level.to_bytes(2, "big") + len(prefixes).to_bytes(4, "big") + b"".join(packed)
+                   + bytes([int(level == 0)]))
+        else:
+            enc = mastic.encode_agg_param(agg_param)
 
         if n and prefixes:
             # both aggregators' prep_init are queued before either result is
@@ -112,23 +149,35 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
             (_msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
             alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
             mask = alive.astype(np.uint8)
-            agg_shares = [mastic.aggregate_device(agg_id, enc, mask) for agg_id in range(2)]
+            if fast and merge is None:
+                raw = [mastic.aggregate_device(agg_id, enc, mask, raw=True) for agg_id in range(2)]
+                agg_shares = None
+            else:
+                agg_shares = [mastic.aggregate_device(agg_id, enc, mask) for agg_id in range(2)]
         else:
             agg_shares = [mastic.agg_init(agg_param) for _ in range(2)]
-        if merge is not None:
-            agg_shares = [merge(a) for a in agg_shares]
-        agg_result = mastic.unshard(agg_param, agg_shares, int(alive.sum()))
+        if agg_shares is None:
+            agg_result = _unshard_raw(mastic, raw, int(alive.sum()))
+        else:
+            if merge is not None:
+                agg_shares = [merge(a) for a in agg_shares]
+            agg_result = mastic.unshard(agg_param, agg_shares, int(alive.sum()))
         prev_agg_params.append(agg_param)
         if trace is not None:
             trace.append(SweepLevel(level, list(prefixes), agg_result, int(alive.sum())))
 
         if level < bits - 1:
             next_prefixes = []
-            for (prefix, count) in zip(prefixes, agg_result):
+            next_packed = []
+            for (i, (prefix, count)) in enumerate(zip(prefixes, agg_result)):
                 if count >= get_threshold(thresholds, prefix):
                     next_prefixes.append(prefix + (False,))
                     next_prefixes.append(prefix + (True,))
+                    if fast:
+                        next_packed.append(_child_packed(packed[i], level + 1, False))
+                        next_packed.append(_child_packed(packed[i], level + 1, True))
             prefixes = next_prefixes
+            packed = next_packed
         else:
             for (prefix, count) in zip(prefixes, agg_result):
                 if count >= get_threshold(thresholds, prefix):

@@ -144,13 +144,14 @@ int mastic_proof_tree(mastic_ctx* ctx, int agg_id, const uint8_t* app_ctx, size_
 /* Frontier cache for level sweeps (the reference's
  * examples.py:37-91 re-evaluates the whole tree at every level).  on = 1
  * enables it, 0 disables it and frees its buffers, -1 leaves it unchanged.
- * With it on, prep_init keeps per report every level's node proofs and payload
- * differences plus the last level's seeds and payloads (HBM: ~48 B per node
- * per report and aggregator); a later prep_init for the same reports, agg_id,
- * verify key and ctx whose tree is the cached tree plus one level (the sweep
- * with no candidate path pruned away) evaluates only that level and re-absorbs
- * the rest from the cache.  Results are identical either way.  *last_hit (if
- * not NULL) = 1 when the last prep_init took the cached path. */
+ * With it on, prep_init keeps per report the two binder sponges' states
+ * (400 B) plus the last level's seeds and payloads; a later prep_init for the
+ * same reports, agg_id, verify key and ctx whose tree is the cached tree plus
+ * one level (the sweep with no candidate path pruned away) evaluates only that
+ * level and resumes the sponges from the cached states (the binder messages
+ * are BFS-ordered, so the cached ones are prefixes of the new ones).  Results
+ * are identical either way.  *last_hit (if not NULL) = 1 when the last
+ * prep_init took the cached path. */
 int mastic_set_frontier_cache(mastic_ctx* ctx, int on, int* last_hit);
 /* Wait for all enqueued work of the ctx. */
 int mastic_synchronize(mastic_ctx* ctx);
@@ -183,7 +184,10 @@ int mastic_shard_batch(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_len, 
 /* ---- measurement hooks (bench) --------------------------------------- */
 /* Device time (ms) of the VIDPF level-eval (AES) kernels and of the
  * binder-absorb kernels during the last prep_init, measured with HIP events on
- * the streams the kernels run on; also their launch counts. */
+ * the streams the kernels run on; also their launch counts.  Timing is kept
+ * per aggregator: "last" is the aggregator of the latest prep_init or
+ * mastic_prep_result call, so both aggregators' prep_init may be queued before
+ * either result is fetched. */
 int mastic_last_timing(mastic_ctx* ctx, double* eval_ms, int* eval_launches, double* absorb_ms,
                        int* absorb_launches, double* total_ms);
 /* HBM work-buffer bytes one report needs during prep_init with this agg

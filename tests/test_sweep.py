@@ -143,3 +143,15 @@ def test_sweep_empty_frontier():
                                  trace=trace) == []
     assert len(trace) == bits and trace[1].prefixes == []
     assert len(m.calls) == 2  # nothing is prepared once the frontier is empty
+
+
+def test_child_packing_matches_pack_path():
+    """The sweep driver's incremental prefix packing equals the MSB-first
+    packing of the whole prefix (PrefixTreeIndex.encode, vidpf.py:33-39)."""
+    from mastic_amd.heavy_hitters import _child_packed
+    from mastic_amd.vdaf import _pack_path
+    rng = random.Random(5)
+    for length in range(1, 260):
+        prefix = tuple(bool(rng.getrandbits(1)) for _ in range(length))
+        for bit in (False, True):
+            assert _child_packed(_pack_path(prefix), length, bit) == _pack_path(prefix + (bit,))
