@@ -325,40 +325,39 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         if (tail_bits && (pfx[i][plen - 1] & ((1u << (8 - tail_bits)) - 1)))
             return fail(c, MASTIC_EINVAL, "prefix with incorrect length");
     }
-    std::vector<std::vector<uint8_t>> sorted_pfx = pfx;
-    std::sort(sorted_pfx.begin(), sorted_pfx.end());
-    if (std::adjacent_find(sorted_pfx.begin(), sorted_pfx.end()) != sorted_pfx.end())
-        return fail(c, MASTIC_EINVAL, "candidate prefixes are non-unique");
-    std::map<std::vector<uint8_t>, int> pfx_index;
-    for (uint64_t i = 0; i < count; i++) pfx_index[pfx[i]] = (int)i;
+    // Sorted candidate order (lexicographic = MSB-first bit order) and the
+    // common-prefix length in bits of each adjacent pair: the distinct
+    // length-m prefixes are the runs of sorted candidates split wherever the
+    // adjacent common prefix is shorter than m, so every level's expanded
+    // nodes, child indices and paths come from O(count) scans (no per-level
+    // sorting, searching or allocation).
+    std::vector<int> order(count);
+    for (uint64_t i = 0; i < count; i++) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return pfx[a] < pfx[b]; });
+    auto bit_of = [&](int s, int l) { return (pfx[order[s]][l / 8] >> (7 - l % 8)) & 1; };
+    std::vector<int> lcp(count, -1);  // lcp[0] = -1: always starts a run
+    for (uint64_t s = 1; s < count; s++) {
+        const std::vector<uint8_t>& a = pfx[order[s - 1]];
+        const std::vector<uint8_t>& b = pfx[order[s]];
+        int bits = 0;
+        size_t k = 0;
+        while (k < plen && a[k] == b[k]) k++;
+        if (k == plen) return fail(c, MASTIC_EINVAL, "candidate prefixes are non-unique");
+        bits = (int)k * 8;
+        if (k < plen) bits += __builtin_clz((unsigned)(a[k] ^ b[k])) - 24;
+        lcp[s] = bits;
+    }
 
     Tree* t = new Tree();
     t->L = level;
     t->n_prefixes = (int)count;
     t->weight_check = enc[len - 1] == 1;
-    // expanded (on-path) nodes per level: distinct length-(l+1) prefixes, sorted
-    auto truncate = [](const std::vector<uint8_t>& v, int nbits) {
-        std::vector<uint8_t> r((nbits + 7) / 8);
-        for (size_t i = 0; i < r.size(); i++) r[i] = v[i];
-        if (nbits % 8) r.back() &= (uint8_t)(0xFF00u >> (nbits % 8));
-        return r;
-    };
-    std::vector<std::vector<std::vector<uint8_t>>> exp(level + 1);
-    for (int l = 0; l < level; l++) {
-        std::vector<std::vector<uint8_t>> v;
-        v.reserve(count);
-        // truncation keeps the MSB-first byte order, so the truncated sorted
-        // list is sorted already (no per-level sort: 255 of them per C3 tree)
-        for (auto& q : sorted_pfx) v.push_back(truncate(q, l + 1));
-        v.erase(std::unique(v.begin(), v.end()), v.end());
-        exp[l] = std::move(v);
-    }
-    std::vector<uint8_t> root;
     size_t total = 0;
+    std::vector<int> run_begin;           // runs of length-l prefixes = parents of level l
+    std::vector<int> gid_next(count, 0);  // run index of each sorted candidate at length l+1
+    run_begin.push_back(0);               // level 0: the root (one run over all candidates)
     for (int l = 0; l <= level; l++) {
-        const std::vector<std::vector<uint8_t>>& parents =
-            l == 0 ? std::vector<std::vector<uint8_t>>{root} : exp[l - 1];
-        const int np = (int)parents.size();
+        const int np = (int)run_begin.size();
         t->n_parents.push_back(np);
         t->poff.push_back(t->parent_node.size());
         if (l > 0) {
@@ -368,25 +367,47 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
             for (int k = 0; k < prev_nodes; k++)
                 if (t->child_exp[prev + k] >= 0) t->parent_node.push_back(k);
         }
-        t->n_exp.push_back(l < level ? (int)exp[l].size() : 0);
+        int n_next = 0;
+        std::vector<int> next_begin;
+        if (l < level) {
+            for (uint64_t s = 0; s < count; s++) {
+                if (lcp[s] < l + 1) {
+                    next_begin.push_back((int)s);
+                    n_next++;
+                }
+                gid_next[s] = n_next - 1;
+            }
+        }
+        t->n_exp.push_back(n_next);
         t->off.push_back(total);
+        const int nb = (l + 1 + 7) / 8;  // path bytes at this level
         for (int pi = 0; pi < np; pi++) {
+            const int b = run_begin[pi];
+            const int e = pi + 1 < np ? run_begin[pi + 1] : (int)count;
+            const std::vector<uint8_t>& rep = pfx[order[b]];
             for (int cbit = 0; cbit < 2; cbit++) {
-                std::vector<uint8_t> path = parents[pi];
-                path.resize((l + 1 + 7) / 8, 0);
-                if (cbit) path[l / 8] |= (uint8_t)(0x80u >> (l % 8));
+                // child cbit exists iff the run's first (cbit 0) / last (cbit 1)
+                // member has that bit at position l
+                const int m = cbit ? e - 1 : b;
+                const bool exists = bit_of(m, l) == cbit;
                 int ce = -1, cp = -1;
-                if (l < level) {
-                    auto f = std::lower_bound(exp[l].begin(), exp[l].end(), path);
-                    if (f != exp[l].end() && *f == path) ce = (int)(f - exp[l].begin());
-                } else {
-                    auto f = pfx_index.find(path);
-                    if (f != pfx_index.end()) cp = f->second;
+                if (exists) {
+                    if (l < level)
+                        ce = gid_next[m];
+                    else
+                        cp = order[m];
                 }
                 t->child_exp.push_back(ce);
                 t->child_pfx.push_back(cp);
+                // path: the parent's l bits, then cbit (bits past l + 1 zero)
                 uint32_t w[8] = {0};
-                for (size_t b = 0; b < path.size(); b++) w[b / 4] |= (uint32_t)path[b] << (8 * (b % 4));
+                for (int bi = 0; bi < nb; bi++) {
+                    uint32_t byte = rep[bi];
+                    const int lo = bi * 8;
+                    if (lo + 8 > l) byte = lo >= l ? 0u : (byte & ((0xFF00u >> (l - lo)) & 0xFFu));
+                    if (cbit && bi == l / 8) byte |= 0x80u >> (l % 8);
+                    w[bi / 4] |= byte << (8 * (bi % 4));
+                }
                 for (int k = 0; k < 8; k++) t->child_path.push_back(w[k]);
             }
         }
@@ -395,6 +416,7 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         t->max_parents = std::max(t->max_parents, np);
         t->max_exp = std::max(t->max_exp, t->n_exp.back());
         if (l > 0) t->interior += np;
+        run_begin.swap(next_begin);
     }
     t->nodes = total;
     const size_t npar = std::max<size_t>(t->parent_node.size(), 1);
