@@ -84,7 +84,7 @@ struct LevelCache {
     std::vector<uint8_t> key;                   // verify key || ctx
     int L = -1;                                 // level of the cached call
     std::vector<int> n_parents;                 // per level 0..L
-    std::vector<uint32_t> paths;                // child paths of levels 0..L (8 words per node)
+    std::vector<uint32_t> paths;                // child paths of level L (8 words per node)
     DevBuf sp;                                  // both binder sponges after levels 0..L (2 x 50 planes)
     DevBuf cs[2], w[2], rootsum;                // last level's seeds/ctrl and payloads; root sum
     int wcur = 0;                               // which cs / w hold the cached level (the other is written)
@@ -888,8 +888,11 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         hit = lc->valid && lc->rep_gen == rep->gen && lc->n == n && lc->stride == stride1 && lc->key == lkey &&
               !t->weight_check && L == lc->L + 1 && (size_t)L <= lc->n_parents.size() &&
               std::equal(t->n_parents.begin(), t->n_parents.begin() + L, lc->n_parents.begin()) &&
-              lc->paths.size() == t->off[L] * 8 &&
-              std::equal(lc->paths.begin(), lc->paths.end(), t->child_path.begin());
+              // level L-1's node paths fix every level above (each level's
+              // parents are the truncations of the next level's nodes), so
+              // they and the node counts decide that the trees agree there
+              lc->paths.size() == (t->off[L] - t->off[L - 1]) * 8 &&
+              std::equal(lc->paths.begin(), lc->paths.end(), t->child_path.begin() + t->off[L - 1] * 8);
         // tiles for every 64-row group of the padded stride: the sponge
         // kernels run over all pl.stride rows, padding included
         const size_t S1 = (size_t)stride1, groups = S1 / 64;
@@ -927,7 +930,8 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         lc->key = lkey;
         lc->L = t->L;
         lc->n_parents.assign(t->n_parents.begin(), t->n_parents.begin() + t->L + 1);
-        lc->paths.assign(t->child_path.begin(), t->child_path.begin() + (t->off[t->L] + 2 * t->n_parents[t->L]) * 8);
+        lc->paths.assign(t->child_path.begin() + t->off[t->L] * 8,
+                         t->child_path.begin() + (t->off[t->L] + 2 * t->n_parents[t->L]) * 8);
     }
     c->last_hit = hit;
     HIPCHK(c, hipEventRecord(t1, c->stream));
@@ -988,7 +992,9 @@ extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_share
             }
         }
     }
-    if (jr_seeds) {
+    if (jr_seeds && !(R.weight_check && p.joint_rand_len > 0)) {
+        memset(jr_seeds, 0, 32 * n);  // no joint rand in this call: the device buffer is all zero
+    } else if (jr_seeds) {
         if ((rc = fetch(c, R.jr_seed, 8, S, js))) return rc;
         for (size_t r = 0; r < n; r++) put_words(jr_seeds + 32 * r, js, S, r, 0, 8);
     }
