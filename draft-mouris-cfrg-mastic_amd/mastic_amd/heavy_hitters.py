@@ -73,6 +73,18 @@ def _unshard_raw(mastic: Mastic, raw_shares, num_measurements):
     return [mastic.decode_result(agg[i + 1:i + k], agg[i].int()) for i in range(0, len(agg), k)]
 
 
+def joint_rand_confirmed(msgs: bytes, jr_seeds_0: bytes, jr_seeds_1: bytes, n: int):
+    """Per report: ``prep_next``'s joint-rand confirmation (mastic.py:369-375)
+    for both aggregators -- the prep message (the seed recomputed from both
+    parts, ``prep_shares_to_prep``) equals each aggregator's own seed."""
+    if n == 0:
+        return np.ones(0, dtype=bool)
+    m = np.frombuffer(msgs, np.uint8, count=32 * n).reshape(n, 32)
+    j0 = np.frombuffer(jr_seeds_0, np.uint8, count=32 * n).reshape(n, 32)
+    j1 = np.frombuffer(jr_seeds_1, np.uint8, count=32 * n).reshape(n, 32)
+    return (m == j0).all(axis=1) & (m == j1).all(axis=1)
+
+
 class SweepLevel:
     """What one level of the sweep did (for callers that want the trace)."""
 
@@ -146,8 +158,12 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                 shares.append(mastic.prep_result(dev, agg_id, enc))
                 if timing is not None:
                     timing.append(mastic.last_timing3())
-            (_msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
+            (msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
             alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
+            if level == 0 and mastic.JOINT_RAND_LEN > 0:
+                # prep_next (mastic.py:364-377, called at examples.py:67): each
+                # aggregator's joint-rand seed must equal the prep message
+                alive &= joint_rand_confirmed(msgs, shares[0][1], shares[1][1], n)
             mask = alive.astype(np.uint8)
             if fast and merge is None:
                 raw = [mastic.aggregate_device(agg_id, enc, mask, raw=True) for agg_id in range(2)]
