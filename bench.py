@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0
 # constructor, level, candidate prefixes, default reports per rank per step.
 CONFIGS = {
     "c2": dict(circuit="Sum", kw=dict(bits=32, max_measurement=255), prefixes=10000, reports=12288,
+               total=1000000, full_job=True,
                desc="C2: Mastic(BITS=32, Sum max=255) prep_init+aggregate, level 31"),
     "c3": dict(circuit="Count", kw=dict(bits=256), prefixes=128, reports=16384,
                desc="C3: Mastic(BITS=256, Count) prep_init+aggregate at level 255 of the threshold-pruned "
@@ -73,9 +74,16 @@ def parse():
                     help="BASELINE config (c2 = the metric's headline config)")
     ap.add_argument("--reports", type=int, default=0, help="reports per rank per step (0 = config default)")
     ap.add_argument("--prefixes", type=int, default=0, help="candidate prefixes (0 = config default)")
+    ap.add_argument("--total-reports", type=int, default=0,
+                    help="reports resident in HBM per rank; steps walk distinct --reports slices of them "
+                         "(0 = config default: 1M for c2)")
+    ap.add_argument("--full-job", type=int, default=-1,
+                    help="also time prep_init+aggregate over all resident reports (-1 = config default)")
     ap.add_argument("--agg-id", type=int, default=0)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU baseline leg")
-    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU baseline pool size (0 = every CPU this process may use, see cpu_pool_size)")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--frontier-cache", type=int, default=1,
                     help="sweep configs: keep each level's binder inputs in HBM (Mastic.set_frontier_cache)")
     return ap.parse_args()
@@ -300,9 +308,9 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
     if rank == 0 and world == 1 and args.cpu_baseline:
         # oracle prep_init (leader) of one report per process at 8 levels spread over the sweep,
         # with the GPU trace's candidate prefixes: a bounded sample of the same workload
-        procs = min(args.cpu_procs, os.cpu_count() or 1)
+        procs = cpu_pool_size(args.cpu_procs)
         lvls = [lv for lv in traces[0] if lv.prefixes][::max(1, len(traces[0]) // 8)][:8]
-        (rn, pub, in0, _in1) = reps.download()
+        (rn, pub, in0, _in1) = reps.view(0, procs).download()
         ps, isz = m.sizes.public_share_size, m.sizes.input_share_size[0]
         spec = (cfg["circuit"], cfg["kw"])
         jobs = []
@@ -328,9 +336,75 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
         dist.destroy_process_group()
 
 
+# ---------------------------------------------------------------- launch
+def launch_command(argv, n_gpus, port):
+    """The torch.distributed.run command that re-runs this script with one
+    rank per GPU (as the driver launches it for N > 1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n_gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_relaunch(args, argv):
+    """--gpus N without a launcher: start N ranks through torch.distributed.run
+    as a child process (before anything touches the GPU) and return its exit
+    code; under a launcher, --gpus must equal WORLD_SIZE."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus > 1:
+            import socket
+            import subprocess
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+            s.close()
+            return subprocess.call(launch_command(argv, args.gpus, port))
+        return None
+    if int(world) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s (launch one rank per GPU)" % (args.gpus, world))
+    return None
+
+
+def cpu_pool_size(requested):
+    """Worker processes for the CPU baseline: the host's CPUs this process may
+    use (affinity), capped by OMP_NUM_THREADS when the box sets it (its CPU
+    share; os.cpu_count() there counts the whole machine) and by --cpu-procs."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    if requested > 0:
+        n = min(n, requested)
+    return max(1, n)
+
+
+def cpu_host_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"cpu_model": model, "host_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
+    if args.launch_probe:  # tests: report the rank layout and exit (no GPU)
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")),
+                          "world": int(os.environ.get("WORLD_SIZE", "1")), "gpus": args.gpus}), flush=True)
+        return 0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -341,33 +415,42 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from mastic_amd import Mastic
-    from mastic_amd.merge import merge_agg_shares
+    from mastic_amd.merge import aggregate_to_tensor, fold_on_gpu, merge_agg_shares
 
     cfg = CONFIGS[args.config]
     n_rep = args.reports or cfg["reports"]
     if cfg.get("sweep"):
         return run_sweep(args, cfg, n_rep, world, rank, local, dist, torch)
     n_pre = args.prefixes or cfg["prefixes"]
+    n_total = max(args.total_reports or cfg.get("total", n_rep), n_rep)
     kw = dict(cfg["kw"])
     bits = kw.pop("bits")
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
-    attrs, alpha_b, betas, nonces, rands = synth(m, cfg, rank, n_rep, n_pre, seed)
+    attrs, alpha_b, betas, nonces, rands = synth(m, cfg, rank, n_total, n_pre, seed)
     vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
     enc_ap = agg_param_bytes(bits - 1, attrs)
-    reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
+    # the whole job's reports resident in HBM (GPU shard); each step runs the
+    # hot path over the next distinct n_rep-report slice of them
+    t_sh = time.perf_counter()
+    reps_all = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
+    m.synchronize()
+    shard_s = time.perf_counter() - t_sh
+    del alpha_b, betas, nonces, rands
+    slices = [reps_all.view(i * n_rep, n_rep) for i in range(n_total // n_rep)]
     (nodes, interior, _maxl) = m.tree_stats(enc_ap)
+    n_elems = len(attrs) * (1 + m.OUTPUT_LEN)
 
-    def step():
+    def step(reps):
         m.prep_init_device(reps, vk, ctx, args.agg_id, enc_ap)
-        agg = m.aggregate_device(args.agg_id, enc_ap, raw=True)
         if world > 1:
-            merge_agg_shares(m, agg, dist)  # RCCL all-gather + on-GPU mod-p fold
-        return agg
+            # agg share folded into HBM, RCCL all-gather, on-GPU mod-p fold
+            return merge_agg_shares(m, aggregate_to_tensor(m, args.agg_id, n_elems), dist)
+        return m.aggregate_device(args.agg_id, enc_ap, raw=True)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(slices[-1 - (i % len(slices))])
     m.synchronize()
     if dist:
         dist.barrier()
@@ -375,8 +458,8 @@ def main():
     t0 = time.perf_counter()
     aes_ms = proof_ms = absorb_ms = total_ms = 0.0
     n_launch = 0
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(slices[k % len(slices)])
         (ea, na_, ep, _np, eb, _nb, t) = m.last_timing3()
         aes_ms += ea
         proof_ms += ep
@@ -423,8 +506,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {
-            "workload": "%s, %d reports x %d prefixes per rank per step, weight check, agg_id %d"
-                        % (cfg["desc"], n_rep, len(attrs), args.agg_id),
+            "workload": "%s, %d reports resident per rank, each step a distinct %d-report slice x %d "
+                        "prefixes, weight check, agg_id %d" % (cfg["desc"], n_total, n_rep, len(attrs), args.agg_id),
             "reports_per_step": n_rep * world,
             "prefixes": len(attrs),
             "nodes_per_report": nodes,
@@ -465,9 +548,52 @@ def main():
                 out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
                 out["roofline"]["traffic_unit"] = "bytes per launch"
 
+    full = cfg.get("full_job", False) if args.full_job < 0 else bool(args.full_job)
+    if full and n_total > n_rep:
+        # the whole resident batch: every slice (the tail too) through prep_init
+        # + fold, the per-slice agg shares merged on the GPU into the job's
+        # agg share (out shares of 1M x 10k prefixes = 160 GB cannot be
+        # materialised at once, so the job is necessarily sliced)
+        bounds = [(i, min(n_rep, n_total - i)) for i in range(0, n_total, n_rep)]
+        tail = reps_all.view(bounds[-1][0], bounds[-1][1]) if bounds[-1][1] != n_rep else None
+        m.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        parts = []
+        for (j, (first, cnt)) in enumerate(bounds):
+            v = slices[j] if cnt == n_rep else tail
+            m.prep_init_device(v, vk, ctx, args.agg_id, enc_ap)
+            parts.append(aggregate_to_tensor(m, args.agg_id, n_elems))
+        job = fold_on_gpu(m, torch.cat(parts), len(parts), n_elems)
+        if world > 1:
+            job = merge_agg_shares(m, job, dist)
+        m.synchronize()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        wall = time.perf_counter() - t1
+        if dist:
+            tt = torch.tensor([wall], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            wall = float(tt.item())
+        out["full_job"] = {
+            "reports_per_rank": n_total,
+            "prefixes": len(attrs),
+            "wall_s": wall,
+            "value": n_total * len(attrs) * world / wall,
+            "unit": "report*prefix/s",
+            "slices": len(bounds),
+            "what": "prep_init (leader) + fold of every resident report, %d slices of <= %d, slice agg shares "
+                    "merged mod p on the GPU (mastic_fold_shares)" % (len(bounds), n_rep),
+        }
+    out["config"]["resident_reports_per_rank"] = n_total
+    out["config"]["shard_s"] = shard_s
+
     if rank == 0 and world == 1 and args.cpu_baseline:
-        procs = min(args.cpu_procs, os.cpu_count() or 1)
-        (rn, pub, in0, in1) = reps.download()
+        procs = cpu_pool_size(args.cpu_procs)
+        (rn, pub, in0, in1) = reps_all.view(0, procs).download()
         ps = m.sizes.public_share_size
         isz = m.sizes.input_share_size[args.agg_id]
         ins = in0 if args.agg_id == 0 else in1
@@ -486,11 +612,13 @@ def main():
             "unit": "report*prefix/s",
             "cores": procs,
             "kind": "port",
-            "sample": "%d reports x %d prefixes, one per process (multiprocessing spawn pool of %d); "
-                      "poc-faithful Python oracle with C AES/TurboSHAKE; %.1f s per report per core "
-                      "(single-core %.0f report*prefix/s); GPU/CPU prep shares bit-identical: %s"
-                      % (procs, len(attrs), procs, per_report, len(attrs) / per_report, parity),
+            "single_process_value": len(attrs) / per_report,
+            "sample": "%d reports x %d prefixes, one per process (multiprocessing spawn pool of %d = the CPUs "
+                      "this process may use); poc-faithful Python oracle with C AES/TurboSHAKE; %.1f s per "
+                      "report per core; GPU/CPU prep shares bit-identical: %s"
+                      % (procs, len(attrs), procs, per_report, parity),
         }
+        out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
     if rank == 0:
         print(json.dumps(out))
@@ -499,4 +627,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    _rc = maybe_relaunch(_args, sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+    sys.exit(main() or 0)

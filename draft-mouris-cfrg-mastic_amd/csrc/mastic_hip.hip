@@ -6,6 +6,7 @@
 #include "mastic_hip.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -22,11 +23,20 @@ namespace {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool own = true;  // false: a view into another buffer (mastic_reports_view)
     ~DevBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && own) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
+        own = true;
+    }
+    void view(const DevBuf& b, size_t off, size_t len) {
+        release();
+        if (!b.p) return;
+        p = (uint8_t*)b.p + off;
+        bytes = len;
+        own = false;
     }
     bool ensure(size_t want) {
         if (want <= bytes && p) return true;
@@ -93,11 +103,14 @@ struct LevelCache {
 
 }  // namespace
 
-static uint64_t g_reports_gen = 0;  // contents generation (frontier-cache key)
+// contents generation (frontier-cache key); contexts may be driven from
+// several threads, so it is atomic
+static std::atomic<uint64_t> g_reports_gen{0};
+static uint64_t next_reports_gen() { return g_reports_gen.fetch_add(1) + 1; }
 struct mastic_reports {
     mastic_ctx* ctx = nullptr;
     size_t n = 0;
-    uint64_t gen = ++g_reports_gen;
+    uint64_t gen = next_reports_gen();
     DevBuf nonces, pub, in0, in1;
 };
 
@@ -109,6 +122,7 @@ struct mastic_ctx {
     hipStream_t stream2 = nullptr;  // binder sponges (overlap the next level's eval)
     hipStream_t stream3 = nullptr;  // node proofs (VALU-only, overlap the LDS-bound AES)
     std::vector<hipEvent_t> sync_ev;
+    hipEvent_t fold_ev = nullptr;  // mastic_fold_shares: producer stream -> stream
     PrefixState pfx_host[PFX_COUNT];
     std::string err;
     uint64_t budget = 0;
@@ -150,6 +164,7 @@ struct mastic_ctx {
         for (auto& x : tm)
             for (auto e : x.ev) (void)hipEventDestroy(e);
         for (auto e : sync_ev) (void)hipEventDestroy(e);
+        if (fold_ev) (void)hipEventDestroy(fold_ev);
         if (stream) (void)hipStreamDestroy(stream);
         if (stream2) (void)hipStreamDestroy(stream2);
         if (stream3) (void)hipStreamDestroy(stream3);
@@ -208,18 +223,29 @@ static std::vector<uint8_t> dst_alg(const uint8_t* ctx, size_t n, int usage, uin
     return d;
 }
 
-// Compute the 12 sponge prefix states for (ctx, verify_key) on the device.
-static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* vk) {
-    static const uint8_t zero_vk[32] = {0};
+// Compute the sponge prefix states for (ctx, verify_key) on the device.  The
+// verify key is XofTurboShake128's seed (u8 length prefix, mastic.py:302-306,
+// 499-510), so any length up to 255 bytes is accepted (the reference's own
+// driver uses 16, examples.py:38,176; VERIFY_KEY_SIZE is 32, mastic.py:73).
+static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, const uint8_t* vk, size_t vk_len) {
     if (ctx_len > 65535 - 12) return fail(c, MASTIC_EINVAL, "ctx too long");
+    if (vk && vk_len > 255) return fail(c, MASTIC_EINVAL, "verify key too long");
     // callers without a verify key (decide, shard, proof tree) never read the
     // two verify-key states (PFX_EVAL, PFX_QUERY: prep_init only), so any
-    // states of the same ctx serve them
-    if (!vk && !c->pfx_key.empty() && c->pfx_key.size() == 32 + ctx_len + 1 &&
-        (ctx_len == 0 || std::equal(app_ctx, app_ctx + ctx_len, c->pfx_key.begin() + 32)))
-        return 0;
-    if (!vk) vk = zero_vk;
-    std::vector<uint8_t> key(vk, vk + 32);
+    // states of the same ctx serve them.  Key layout: u8(len) || vk || ctx || 1.
+    if (!vk && !c->pfx_key.empty()) {
+        const size_t kl = c->pfx_key[0];
+        if (c->pfx_key.size() == 1 + kl + ctx_len + 1 &&
+            (ctx_len == 0 || std::equal(app_ctx, app_ctx + ctx_len, c->pfx_key.begin() + 1 + kl)))
+            return 0;
+    }
+    static const uint8_t zero_vk[32] = {0};
+    if (!vk) {
+        vk = zero_vk;
+        vk_len = 32;
+    }
+    std::vector<uint8_t> key(1, (uint8_t)vk_len);
+    key.insert(key.end(), vk, vk + vk_len);
     key.insert(key.end(), app_ctx, app_ctx + ctx_len);
     key.push_back(1);  // never equal to the empty "none" key
     if (key == c->pfx_key) return 0;  // same verify key and ctx as the states already in pfx
@@ -241,8 +267,8 @@ static int build_prefixes(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len,
     xof_ts(PFX_NODE, dst(app_ctx, ctx_len, 9), 16, nullptr);
     xof_ts(PFX_ONEHOT, dst_alg(app_ctx, ctx_len, 6, ID), 0, nullptr);
     xof_ts(PFX_PAYLOAD, dst_alg(app_ctx, ctx_len, 7, ID), 0, nullptr);
-    xof_ts(PFX_EVAL, dst_alg(app_ctx, ctx_len, 8, ID), 32, vk);
-    xof_ts(PFX_QUERY, dst_alg(app_ctx, ctx_len, 2, ID), 32, vk);
+    xof_ts(PFX_EVAL, dst_alg(app_ctx, ctx_len, 8, ID), (int)vk_len, vk);
+    xof_ts(PFX_QUERY, dst_alg(app_ctx, ctx_len, 2, ID), (int)vk_len, vk);
     xof_ts(PFX_PROOF_SHARE, dst_alg(app_ctx, ctx_len, 1, ID), 32, nullptr);
     xof_ts(PFX_JR_PART, dst_alg(app_ctx, ctx_len, 4, ID), 32, nullptr);
     xof_ts(PFX_JR_SEED, dst_alg(app_ctx, ctx_len, 3, ID), 0, nullptr);
@@ -828,7 +854,7 @@ static uint64_t default_budget(mastic_ctx* c) {
     return (uint64_t)(freeb * 0.75);
 }
 
-extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_t verify_key[32],
+extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_t* verify_key, size_t vk_len,
                                 const uint8_t* app_ctx, size_t ctx_len, int agg_id, const uint8_t* enc_agg_param,
                                 size_t agg_param_len) {
     DeviceScope ds_(c);
@@ -836,12 +862,14 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     if (agg_id != 0 && agg_id != 1) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     if ((agg_id == 0 && !rep->in0.p) || (agg_id == 1 && !rep->in1.p))
         return fail(c, MASTIC_EINVAL, "reports hold no input shares for this aggregator");
-    if (!verify_key) return fail(c, MASTIC_EINVAL, "verify key required");
+    if (!verify_key && vk_len) return fail(c, MASTIC_EINVAL, "verify key required");
+    static const uint8_t empty_vk[1] = {0};
+    if (!verify_key) verify_key = empty_vk;
     c->tcur = agg_id;
     Tree* t = nullptr;
     int rc = build_tree(c, enc_agg_param, agg_param_len, &t);
     if (rc) return rc;
-    if ((rc = build_prefixes(c, app_ctx, ctx_len, verify_key))) return rc;
+    if ((rc = build_prefixes(c, app_ctx, ctx_len, verify_key, vk_len))) return rc;
     const McParams& p = c->p;
     WorkLayout wl = work_layout(p, t);
     const size_t n = rep->n;
@@ -879,7 +907,8 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     // frontier cache (one-chunk batches with tiled binder buffers only)
     LevelCache* lc = nullptr;
     bool hit = false;
-    std::vector<uint8_t> lkey(verify_key, verify_key + 32);
+    std::vector<uint8_t> lkey(1, (uint8_t)vk_len);
+    lkey.insert(lkey.end(), verify_key, verify_key + vk_len);
     lkey.insert(lkey.end(), app_ctx, app_ctx + ctx_len);
     if (c->frontier_cache && c->binder_tiled && chunk >= n) {
         lc = &c->lc[agg_id];
@@ -1010,6 +1039,29 @@ extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_share
     return 0;
 }
 
+// Fold of the out shares of the last prep_init of agg_id into dagg (device).
+static int aggregate_impl(mastic_ctx* c, int agg_id, const uint8_t* valid, uint32_t* dagg) {
+    Result& R = c->res[agg_id];
+    const McParams& p = c->p;
+    const size_t rows = (size_t)R.n_prefixes * (1 + p.output_len);
+    const uint8_t* dv = nullptr;
+    if (valid && R.n) {
+        if (!c->agg_valid.ensure(R.n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        HIPCHK(c, hipMemcpyAsync(c->agg_valid.p, valid, R.n, hipMemcpyHostToDevice, c->stream));
+        dv = c->agg_valid.as<uint8_t>();
+    }
+    if (rows) {
+        if (p.field == 64)
+            hipLaunchKernelGGL(k_fold<F64>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
+                               (int)R.stride, dv, dagg);
+        else
+            hipLaunchKernelGGL(k_fold<F128>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
+                               (int)R.stride, dv, dagg);
+        HIPCHK(c, hipGetLastError());
+    }
+    return 0;
+}
+
 extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid, uint8_t* agg_share) {
     DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
@@ -1017,35 +1069,38 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
     const McParams& p = c->p;
     const size_t rows = (size_t)R.n_prefixes * (1 + p.output_len);
-    DevBuf& dvalid = c->agg_valid;
-    DevBuf& dagg = c->agg_out;
-    const uint8_t* dv = nullptr;
-    if (valid && R.n) {
-        if (!dvalid.ensure(R.n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
-        HIPCHK(c, hipMemcpyAsync(dvalid.p, valid, R.n, hipMemcpyHostToDevice, c->stream));
-        dv = dvalid.as<uint8_t>();
-    }
-    if (!dagg.ensure(std::max<size_t>(rows, 1) * p.w32 * 4)) return fail(c, MASTIC_ENOMEM, "out of device memory");
-    if (rows) {
-        if (p.field == 64)
-            hipLaunchKernelGGL(k_fold<F64>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
-                               (int)R.stride, dv, dagg.as<uint32_t>());
-        else
-            hipLaunchKernelGGL(k_fold<F128>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
-                               (int)R.stride, dv, dagg.as<uint32_t>());
-        HIPCHK(c, hipGetLastError());
-    }
-    if (agg_share && rows) HIPCHK(c, hipMemcpyAsync(agg_share, dagg.p, rows * p.w32 * 4, hipMemcpyDeviceToHost, c->stream));
+    if (!c->agg_out.ensure(std::max<size_t>(rows, 1) * p.w32 * 4)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+    int rc = aggregate_impl(c, agg_id, valid, c->agg_out.as<uint32_t>());
+    if (rc) return rc;
+    if (agg_share && rows)
+        HIPCHK(c, hipMemcpyAsync(agg_share, c->agg_out.p, rows * p.w32 * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }
 
+extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share) {
+    DeviceScope ds_(c);
+    if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
+    Result& R = c->res[agg_id];
+    if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
+    const size_t rows = (size_t)R.n_prefixes * (1 + c->p.output_len);
+    if (rows && !dev_agg_share) return fail(c, MASTIC_EINVAL, "null agg share buffer");
+    int rc = aggregate_impl(c, agg_id, valid, (uint32_t*)dev_agg_share);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's stream (e.g. RCCL's) reads it next
+    return 0;
+}
+
 extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t n_shares, size_t n_elems,
-                                  void* dev_out) {
+                                  void* dev_out, void* producer_stream) {
     DeviceScope ds_(c);
     if (!c || (!dev_shares && n_shares) || !dev_out) return MASTIC_EINVAL;
     if (n_elems == 0) return 0;
-    HIPCHK(c, hipDeviceSynchronize());  // the shares may come from another stream (RCCL)
+    // the shares were written on the caller's stream (e.g. an RCCL all-gather):
+    // order the fold after that stream's work with an event, not a device sync
+    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->fold_ev, (hipStream_t)producer_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->fold_ev, 0));
     const dim3 grid((unsigned)((n_elems + 255) / 256));
     if (c->p.field == 64)
         hipLaunchKernelGGL(k_fold_shares<F64>, grid, dim3(256), 0, c->stream, (const uint32_t*)dev_shares,
@@ -1072,7 +1127,7 @@ extern "C" int mastic_proof_tree(mastic_ctx* c, int agg_id, const uint8_t* app_c
     if (n_nodes != total) return fail(c, MASTIC_EINVAL, "proof tree has incorrect size");
     if (n == 0) return 0;
     if (n > (size_t)INT32_MAX / 2) return fail(c, MASTIC_EINVAL, "batch too large for a proof tree");
-    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr);
+    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr, 0);
     if (rc) return rc;
     DevBuf nodes;
     if (!nodes.ensure(total * 32)) return fail(c, MASTIC_ENOMEM, "out of device memory (proof tree)");
@@ -1163,7 +1218,7 @@ extern "C" int mastic_work_bytes(mastic_ctx* c, const uint8_t* enc, size_t len, 
     return 0;
 }
 
-extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t verify_key[32], const uint8_t* app_ctx,
+extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t* verify_key, size_t vk_len, const uint8_t* app_ctx,
                                       size_t ctx_len, int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len,
                                       size_t n, const uint8_t* nonces, const uint8_t* public_shares,
                                       const uint8_t* input_shares, uint8_t* prep_shares_out, uint8_t* jr_seeds_out,
@@ -1176,7 +1231,7 @@ extern "C" int mastic_prep_init_batch(mastic_ctx* c, const uint8_t verify_key[32
     if (rc) return rc;
     rc = mastic_reports_upload(rep, nonces, public_shares, agg_id == 0 ? input_shares : nullptr,
                                agg_id == 1 ? input_shares : nullptr);
-    if (!rc) rc = mastic_prep_init(c, rep, verify_key, app_ctx, ctx_len, agg_id, enc_agg_param, agg_param_len);
+    if (!rc) rc = mastic_prep_init(c, rep, verify_key, vk_len, app_ctx, ctx_len, agg_id, enc_agg_param, agg_param_len);
     if (!rc) rc = mastic_prep_result(c, agg_id, prep_shares_out, jr_seeds_out, out_shares_out, status_out);
     mastic_reports_destroy(rep);
     return rc;
@@ -1192,7 +1247,7 @@ extern "C" int mastic_decide_batch(mastic_ctx* c, const uint8_t* app_ctx, size_t
     int rc = build_tree(c, enc, len, &t);
     if (rc) return rc;
     if (n == 0) return 0;
-    if ((rc = build_prefixes(c, app_ctx, ctx_len, nullptr))) return rc;
+    if ((rc = build_prefixes(c, app_ctx, ctx_len, nullptr, 0))) return rc;
     const McParams& p = c->p;
     const size_t psz = mc_prep_share_size(p, t->weight_check);
     const size_t stride = round_up(n, 64);
@@ -1235,6 +1290,24 @@ extern "C" int mastic_reports_create(mastic_ctx* c, size_t n, mastic_reports** o
     return 0;
 }
 
+extern "C" int mastic_reports_view(mastic_reports* rep, size_t first, size_t count, mastic_reports** out) {
+    DeviceScope ds_(rep ? rep->ctx : nullptr);
+    if (!rep || !out) return MASTIC_EINVAL;
+    mastic_ctx* c = rep->ctx;
+    if (first > rep->n || count > rep->n - first) return fail(c, MASTIC_EINVAL, "view out of range");
+    const McParams& p = c->p;
+    mastic_reports* r = new mastic_reports();
+    r->ctx = c;
+    r->n = count;
+    const size_t ps = mc_public_share_size(p), i0 = mc_input_share_size(p, 0), i1 = mc_input_share_size(p, 1);
+    r->nonces.view(rep->nonces, 16 * first, 16 * count);
+    r->pub.view(rep->pub, ps * first, ps * count);
+    r->in0.view(rep->in0, i0 * first, i0 * count);
+    r->in1.view(rep->in1, i1 * first, i1 * count);
+    *out = r;
+    return 0;
+}
+
 extern "C" void mastic_reports_destroy(mastic_reports* r) {
     DeviceScope ds_(r ? r->ctx : nullptr);
     delete r;
@@ -1248,7 +1321,7 @@ extern "C" int mastic_reports_upload(mastic_reports* r, const uint8_t* nonces, c
     mastic_ctx* c = r->ctx;
     const McParams& p = c->p;
     const size_t n = r->n;
-    r->gen = ++g_reports_gen;
+    r->gen = next_reports_gen();
     if (nonces) HIPCHK(c, hipMemcpy(r->nonces.p, nonces, 16 * n, hipMemcpyHostToDevice));
     if (pub) HIPCHK(c, hipMemcpy(r->pub.p, pub, (size_t)mc_public_share_size(p) * n, hipMemcpyHostToDevice));
     if (in0) {
@@ -1359,10 +1432,10 @@ extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx,
     DeviceScope ds_(rep ? rep->ctx : nullptr);
     if (!rep) return MASTIC_EINVAL;
     mastic_ctx* c = rep->ctx;
-    rep->gen = ++g_reports_gen;
+    rep->gen = next_reports_gen();
     if (rep->n == 0) return 0;
     if (!alphas || !nonces || !rands || (!betas && c->p.meas_len > 0)) return fail(c, MASTIC_EINVAL, "null input");
-    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr);
+    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr, 0);
     if (rc) return rc;
     return c->p.field == 64 ? shard_impl<F64>(c, rep, alphas, betas, nonces, rands)
                             : shard_impl<F128>(c, rep, alphas, betas, nonces, rands);
@@ -1467,9 +1540,15 @@ extern "C" void mastic_ctx_destroy(mastic_ctx* c) {
 extern "C" const char* mastic_last_error(const mastic_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
 
 extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
+    DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     if (on >= 0) {
         c->frontier_cache = on != 0;
+        if (!on) {
+            // queued kernels may still read the cache buffers
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->stream2);
+        }
         if (!on)
             for (auto& x : c->lc) {
                 x.drop();

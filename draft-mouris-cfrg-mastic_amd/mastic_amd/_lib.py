@@ -30,6 +30,7 @@ EXPORTS = [
     "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
     "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
     "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
+    "mastic_aggregate_device", "mastic_reports_view",
 ]
 
 
@@ -107,17 +108,19 @@ def lib():
                     "mastic_reports_upload": (i32, [P, P, P, P, P]),
                     "mastic_reports_download": (i32, [P, P, P, P, P]),
                     "mastic_reports_shard": (i32, [P, u8p, sz, P, P, P, P]),
-                    "mastic_prep_init": (i32, [P, P, u8p, u8p, sz, i32, u8p, sz]),
+                    "mastic_prep_init": (i32, [P, P, u8p, sz, u8p, sz, i32, u8p, sz]),
                     "mastic_prep_result": (i32, [P, i32, P, P, P, P]),
                     "mastic_aggregate": (i32, [P, i32, P, P]),
                     "mastic_synchronize": (i32, [P]),
-                    "mastic_prep_init_batch": (i32, [P, u8p, u8p, sz, i32, u8p, sz, sz, P, P, P, P, P, P, P]),
+                    "mastic_prep_init_batch": (i32, [P, u8p, sz, u8p, sz, i32, u8p, sz, sz, P, P, P, P, P, P, P]),
                     "mastic_decide_batch": (i32, [P, u8p, sz, u8p, sz, sz, P, P, P, P]),
                     "mastic_shard_batch": (i32, [P, u8p, sz, sz, P, P, P, P, P, P, P]),
                     "mastic_last_timing": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
-                    "mastic_fold_shares": (i32, [P, P, sz, sz, P]),
+                    "mastic_fold_shares": (i32, [P, P, sz, sz, P, P]),
+                    "mastic_aggregate_device": (i32, [P, i32, P, P]),
+                    "mastic_reports_view": (i32, [P, sz, sz, ctypes.POINTER(P)]),
                     "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3
                                             + [ctypes.POINTER(ctypes.c_double)]),
                     "mastic_work_bytes": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64)]),

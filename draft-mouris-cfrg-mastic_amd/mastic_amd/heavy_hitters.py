@@ -55,9 +55,9 @@ def _child_packed(packed: bytes, level: int, bit: bool) -> bytes:
 
 
 def _unshard_raw(mastic: Mastic, raw_shares, num_measurements):
-    """``mastic.unshard`` (mastic.py:399-411) on the two aggregators'
-    encode_vec agg shares, summed as integers mod p (same result, without a
-    field object per share element)."""
+    """``mastic.unshard`` (mastic.py:399-411) on encode_vec agg shares (the
+    two aggregators', or one already-merged total), summed as integers mod p
+    (same result, without a field object per share element)."""
     f = mastic.field
     enc = f.ENCODED_SIZE
     if enc == 8:
@@ -68,7 +68,7 @@ def _unshard_raw(mastic: Mastic, raw_shares, num_measurements):
     for v in vecs:
         if v and max(v) >= p:
             raise ValueError("encoded element out of range")
-    agg = [f((a + b) % p) for (a, b) in zip(*vecs)]
+    agg = [f(sum(col) % p) for col in zip(*vecs)]
     k = 1 + mastic.OUTPUT_LEN
     return [mastic.decode_result(agg[i + 1:i + k], agg[i].int()) for i in range(0, len(agg), k)]
 
@@ -103,7 +103,7 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     ``(nonce, public_share, input_shares)`` tuples or a device-resident
     :class:`~mastic_amd.vdaf.Reports` batch holding both input shares
     (``Mastic.reports_shard`` / ``reports_upload``).  ``verify_key`` defaults
-    to fresh randomness, as in the reference.  If ``trace`` is a list, one
+    to 16 fresh random bytes, as in the reference (examples.py:38).  If ``trace`` is a list, one
     :class:`SweepLevel` per level is appended to it.  ``merge`` maps this
     rank's agg share (list of field elements) to the job-wide one (all
     ranks call it at every level, in the same order).  If ``timing`` is a
@@ -117,7 +117,7 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
         mastic.set_frontier_cache(frontier_cache)
     if verify_key is None:
         import os
-        verify_key = os.urandom(mastic.VERIFY_KEY_SIZE)
+        verify_key = os.urandom(16)  # gen_rand(16), examples.py:38
     if isinstance(reports, (list, tuple)):
         if len(reports) == 0:
             dev = None
@@ -145,6 +145,9 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
         else:
             enc = mastic.encode_agg_param(agg_param)
 
+        device_merge = fast and merge is not None and hasattr(merge, "total")
+        n_elems = len(prefixes) * (1 + mastic.OUTPUT_LEN) if device_merge else 0
+        raw = agg_shares = None
         if n and prefixes:
             # both aggregators' prep_init are queued before either result is
             # fetched, so the host work of the second overlaps the GPU run of
@@ -165,14 +168,18 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                 # aggregator's joint-rand seed must equal the prep message
                 alive &= joint_rand_confirmed(msgs, shares[0][1], shares[1][1], n)
             mask = alive.astype(np.uint8)
-            if fast and merge is None:
+            if device_merge:
+                # both shares folded, gathered and merged in HBM (one RCCL call)
+                raw = [merge.total(n_elems, mask)]
+            elif fast and merge is None:
                 raw = [mastic.aggregate_device(agg_id, enc, mask, raw=True) for agg_id in range(2)]
-                agg_shares = None
             else:
                 agg_shares = [mastic.aggregate_device(agg_id, enc, mask) for agg_id in range(2)]
+        elif device_merge:
+            raw = [merge.total(n_elems, have_results=False)]  # same collectives on every rank
         else:
             agg_shares = [mastic.agg_init(agg_param) for _ in range(2)]
-        if agg_shares is None:
+        if raw is not None:
             agg_result = _unshard_raw(mastic, raw, int(alive.sum()))
         else:
             if merge is not None:

@@ -6,10 +6,20 @@ aggregate share: one all-gather (RCCL over xGMI with the "nccl" backend)
 into a rank-ordered buffer, then a GF(p) sum on the GPU
 (``mastic_fold_shares``) — RCCL's integer sum is not field addition.
 Mirrors ``Mastic.merge`` (poc/mastic.py:390-397).
+
+The shares stay in HBM from the fold of the out shares
+(``mastic_aggregate_device``) through the all-gather to the GF(p) merge;
+the fold is ordered after the all-gather by an event on the stream RCCL ran
+on (torch's current stream), not by a device-wide synchronisation.
 """
 import ctypes
 
 from . import _lib
+
+
+def _current_stream_handle():
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
 def gather_shares(local, dist):
@@ -21,34 +31,84 @@ def gather_shares(local, dist):
     return out
 
 
-def fold_on_gpu(m, gathered, world, n_elems):
-    """merged[e] = sum_s gathered[s][e] mod p, computed by the HIP kernel."""
+def fold_on_gpu(m, shares, n_shares, n_elems):
+    """merged[e] = sum_s shares[s][e] mod p, computed by the HIP kernel.
+    ``shares`` is a uint8 device tensor of n_shares x n_elems encode_vec
+    elements, written on torch's current stream."""
     import torch
-    merged = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device=gathered.device)
-    torch.cuda.synchronize()
-    rc = _lib.lib().mastic_fold_shares(m._ctx, ctypes.c_void_p(gathered.data_ptr()), world, n_elems,
-                                       ctypes.c_void_p(merged.data_ptr()))
+    merged = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device=shares.device)
+    rc = _lib.lib().mastic_fold_shares(m._ctx, ctypes.c_void_p(shares.data_ptr()), n_shares, n_elems,
+                                       ctypes.c_void_p(merged.data_ptr()), _current_stream_handle())
     if rc != 0:
         raise _lib.MasticError(rc, "mastic_fold_shares failed")
     return merged
 
 
-def merge_agg_shares(m, agg_share, dist):
-    """Rank-local agg share (list of field elements, or its encode_vec bytes)
-    -> job-wide agg share (uint8 device tensor in encode_vec order) on every rank."""
+def aggregate_to_tensor(m, agg_id, n_elems, valid=None, out=None):
+    """The GPU fold of agg_id's last prep_init out shares, left in HBM as a
+    uint8 tensor (``mastic_aggregate_device``)."""
+    import numpy as np
     import torch
-    raw = bytes(agg_share) if isinstance(agg_share, (bytes, bytearray)) else m.field.encode_vec(agg_share)
-    local = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    if out is None:
+        out = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device="cuda")
+    v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
+    rc = _lib.lib().mastic_aggregate_device(m._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(out.data_ptr()))
+    if rc != 0:
+        raise _lib.MasticError(rc, "mastic_aggregate_device failed")
+    return out
+
+
+def merge_agg_shares(m, agg_share, dist):
+    """Rank-local agg share (a uint8 device tensor, its encode_vec bytes, or a
+    list of field elements) -> job-wide agg share (uint8 device tensor in
+    encode_vec order) on every rank."""
+    import torch
+    if isinstance(agg_share, torch.Tensor):
+        local = agg_share
+    else:
+        raw = bytes(agg_share) if isinstance(agg_share, (bytes, bytearray)) else m.field.encode_vec(agg_share)
+        local = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
     gathered = gather_shares(local, dist)
-    return fold_on_gpu(m, gathered, dist.get_world_size(), len(raw) // m.field.ENCODED_SIZE)
+    return fold_on_gpu(m, gathered, dist.get_world_size(), local.numel() // m.field.ENCODED_SIZE)
+
+
+class SweepMerge:
+    """Per-level merge for the sweep driver (heavy_hitters.compute_heavy_hitters)
+    on N ranks.  ``total`` folds both aggregators' out shares on this rank's
+    GPU into one device buffer [agg 0 | agg 1], all-gathers it (one RCCL call
+    per level), and sums the 2 x world shares mod p on the GPU: that is the
+    collector's ``unshard`` merge (mastic.py:399-411) of the job-wide agg
+    shares, so only the final aggregate (len(prefixes) x (1 + OUTPUT_LEN)
+    elements) comes back to the host for the pruning decision.
+
+    Calling the object maps a list of field elements to the job-wide list (the
+    per-share form, kept for drivers that merge shares one by one)."""
+
+    def __init__(self, m, dist):
+        self.m = m
+        self.dist = dist
+
+    def total(self, n_elems, valid=None, have_results=True) -> bytes:
+        import torch
+        m = self.m
+        enc = m.field.ENCODED_SIZE
+        if n_elems == 0:
+            return b""
+        local = torch.zeros(2 * n_elems * enc, dtype=torch.uint8, device="cuda")
+        if have_results:  # a rank with no reports contributes zero shares (agg_init)
+            for agg_id in range(2):
+                aggregate_to_tensor(m, agg_id, n_elems, valid, out=local[agg_id * n_elems * enc:])
+        gathered = gather_shares(local, self.dist)
+        merged = fold_on_gpu(m, gathered, 2 * self.dist.get_world_size(), n_elems)
+        return merged.cpu().numpy().tobytes()
+
+    def __call__(self, agg_share):
+        if len(agg_share) == 0:
+            return agg_share
+        merged = merge_agg_shares(self.m, agg_share, self.dist)
+        return self.m.field.decode_vec(merged.cpu().numpy().tobytes())
 
 
 def merge_field_shares(m, dist):
-    """``merge`` callback for the sweep driver (heavy_hitters.compute_heavy_hitters):
-    rank-local agg share -> job-wide agg share, both as lists of field elements."""
-    def merge(agg_share):
-        if len(agg_share) == 0:
-            return agg_share
-        merged = merge_agg_shares(m, agg_share, dist)
-        return m.field.decode_vec(merged.cpu().numpy().tobytes())
-    return merge
+    """``merge`` for the sweep driver: a :class:`SweepMerge`."""
+    return SweepMerge(m, dist)

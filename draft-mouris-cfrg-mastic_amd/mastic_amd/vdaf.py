@@ -191,8 +191,7 @@ class Mastic:
         enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
         (level, count, wc) = self._agg_param_header(enc)
         n = len(nonces) // 16
-        if len(verify_key) != self.VERIFY_KEY_SIZE:
-            raise ValueError("verify key has incorrect length")
+        self._check_verify_key(verify_key)
         if len(public_shares) != n * self.sizes.public_share_size:
             raise ValueError("public shares have incorrect length")
         if len(input_shares) != n * self.sizes.input_share_size[agg_id]:
@@ -203,7 +202,7 @@ class Mastic:
         out = np.empty(n * ow, np.uint8) if want_out_shares else None
         st = np.empty(n, np.int32)
         _check(self._ctx, _lib.lib().mastic_prep_init_batch(
-            self._ctx, verify_key, ctx, len(ctx), agg_id, enc, len(enc), n, _lib.buf(nonces),
+            self._ctx, verify_key, len(verify_key), ctx, len(ctx), agg_id, enc, len(enc), n, _lib.buf(nonces),
             _lib.buf(public_shares), _lib.buf(input_shares), _lib.buf(ps), _lib.buf(js), _lib.buf(out),
             _lib.buf(st)))
         return (ps.tobytes(), js.tobytes(), None if out is None else out.tobytes(), st)
@@ -222,6 +221,12 @@ class Mastic:
             self._ctx, ctx, len(ctx), enc, len(enc), n, _lib.buf(prep_shares_0), _lib.buf(prep_shares_1),
             _lib.buf(msgs), _lib.buf(valid)))
         return (msgs.tobytes(), valid)
+
+    def aggregate_to(self, agg_id: int, valid, dev_ptr: int):
+        """``mastic_aggregate_device``: fold into caller-owned device memory
+        (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM."""
+        v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
+        _check(self._ctx, _lib.lib().mastic_aggregate_device(self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr)))
 
     def aggregate_device(self, agg_id: int, agg_param, valid=None, raw=False):
         """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU
@@ -252,8 +257,9 @@ class Mastic:
     def prep_init_device(self, reports, verify_key: bytes, ctx: bytes, agg_id: int, agg_param):
         """Enqueue prep_init for resident reports; results stay in HBM."""
         enc = self.encode_agg_param(agg_param) if not isinstance(agg_param, (bytes, bytearray)) else bytes(agg_param)
-        _check(self._ctx, _lib.lib().mastic_prep_init(self._ctx, reports._ptr, verify_key, ctx, len(ctx), agg_id,
-                                                      enc, len(enc)))
+        self._check_verify_key(verify_key)
+        _check(self._ctx, _lib.lib().mastic_prep_init(self._ctx, reports._ptr, verify_key, len(verify_key), ctx,
+                                                      len(ctx), agg_id, enc, len(enc)))
 
     def prep_result(self, reports, agg_id: int, agg_param, want_out_shares=False):
         """Wire results of the last prep_init_device for agg_id:
@@ -330,6 +336,16 @@ class Mastic:
         v = ctypes.c_uint64()
         _check(self._ctx, _lib.lib().mastic_work_bytes(self._ctx, enc, len(enc), ctypes.byref(v)))
         return v.value
+
+    @staticmethod
+    def _check_verify_key(verify_key):
+        """The verify key is XofTurboShake128's seed, length-prefixed with one
+        byte (mastic.py:302-306,499-510): the poc accepts any length below 256
+        (its driver passes 16 bytes, examples.py:38,176)."""
+        if not isinstance(verify_key, (bytes, bytearray)):
+            raise TypeError("verify key must be bytes")
+        if len(verify_key) > 255:
+            raise ValueError("verify key has incorrect length")
 
     @staticmethod
     def _agg_param_header(enc: bytes):
@@ -534,9 +550,21 @@ class Reports:
 
     def __init__(self, mastic, n):
         self._m = mastic
+        self._parent = None
         self._ptr = ctypes.c_void_p()
         _check(mastic._ctx, _lib.lib().mastic_reports_create(mastic._ctx, n, ctypes.byref(self._ptr)))
         self.n = n
+
+    def view(self, first: int, count: int):
+        """Reports first..first+count-1 of this batch, sharing its HBM
+        (``mastic_reports_view``); keeps this batch alive."""
+        v = Reports.__new__(Reports)
+        v._m = self._m
+        v._ptr = ctypes.c_void_p()
+        _check(self._m._ctx, _lib.lib().mastic_reports_view(self._ptr, first, count, ctypes.byref(v._ptr)))
+        v.n = count
+        v._parent = self
+        return v
 
     def download(self):
         m = self._m

@@ -102,6 +102,10 @@ int mastic_reports_upload(mastic_reports* rep, const uint8_t* nonces, const uint
                           const uint8_t* input_shares0, const uint8_t* input_shares1);
 int mastic_reports_download(mastic_reports* rep, uint8_t* nonces, uint8_t* public_shares,
                             uint8_t* input_shares0, uint8_t* input_shares1);
+/* A batch of `count` reports starting at report `first` of `rep`, sharing its
+ * HBM (no copy).  It must be destroyed before `rep`; writing to either
+ * (upload / shard) changes both. */
+int mastic_reports_view(mastic_reports* rep, size_t first, size_t count, mastic_reports** out);
 /* Client shard on the GPU (Mastic.shard).  alphas n*ceil(bits/8) MSB-first,
  * betas n*meas_len*field_bytes = the FLP-encoded measurement (Valid.encode),
  * nonces n*16, rands n*rand_size. */
@@ -110,10 +114,14 @@ int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx, size_t ctx
 
 /* ---- aggregator preparation ----------------------------------------- */
 /* Enqueue prep_init for every report of `rep` as aggregator agg_id.
+ * verify_key is verify_key_len (0..255) bytes: it is XofTurboShake128's seed
+ * (length-prefixed, mastic.py:302-306,499-510), so the reference driver's
+ * 16-byte key (examples.py:38,176) and VERIFY_KEY_SIZE = 32 both work.
  * enc_agg_param is Mastic.encode_agg_param's output.  Results stay in HBM
  * (one result slot per agg_id) until read or aggregated. */
-int mastic_prep_init(mastic_ctx* ctx, mastic_reports* rep, const uint8_t verify_key[32], const uint8_t* app_ctx,
-                     size_t ctx_len, int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len);
+int mastic_prep_init(mastic_ctx* ctx, mastic_reports* rep, const uint8_t* verify_key, size_t verify_key_len,
+                     const uint8_t* app_ctx, size_t ctx_len, int agg_id, const uint8_t* enc_agg_param,
+                     size_t agg_param_len);
 /* Copy results of the last mastic_prep_init for agg_id (blocks).  Any output
  * may be NULL.  prep_shares n*prep_share_size[weight_check] (wire encoding,
  * mastic.py:543-552); jr_seeds n*32 (zero when not applicable);
@@ -125,11 +133,19 @@ int mastic_prep_result(mastic_ctx* ctx, int agg_id, uint8_t* prep_shares, uint8_
  * valid[i] != 0 (valid == NULL: all) into agg_share
  * (len(prefixes)*(1+output_len)*field_bytes, encode_vec). */
 int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t* agg_share);
+/* mastic_aggregate into a caller-owned DEVICE buffer of the ctx's GPU (same
+ * layout), e.g. the send buffer of an RCCL all-gather: the share never
+ * leaves HBM.  Returns when the buffer is written. */
+int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share);
 /* Multi-GPU merge (Mastic.merge, mastic.py:390-397) of n_shares agg shares
  * of n_elems elements each, all in DEVICE memory of the ctx's GPU (e.g. the
  * output of an RCCL all-gather): dev_out[e] = sum_s dev_shares[s][e] mod p.
- * Elements are in encode_vec byte order. */
-int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares, size_t n_elems, void* dev_out);
+ * Elements are in encode_vec byte order.  producer_stream is the hipStream_t
+ * the shares were written on (NULL = the null stream): the fold is ordered
+ * after that stream's queued work by an event.  Returns when dev_out is
+ * written. */
+int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares, size_t n_elems, void* dev_out,
+                       void* producer_stream);
 /* VIDPF-proof aggregation mode (draft-mouris-cfrg-mastic.md, "Plain
  * Heavy-Hitters with VIDPF-Proof Aggregation"; no poc code or wire format in
  * the reference): Merkle tree over the eval proofs of the last prep_init of
@@ -157,8 +173,8 @@ int mastic_set_frontier_cache(mastic_ctx* ctx, int on, int* last_hit);
 int mastic_synchronize(mastic_ctx* ctx);
 
 /* One-shot host-buffer form of upload + prep_init + prep_result. */
-int mastic_prep_init_batch(mastic_ctx* ctx, const uint8_t verify_key[32], const uint8_t* app_ctx, size_t ctx_len,
-                           int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len, size_t n,
+int mastic_prep_init_batch(mastic_ctx* ctx, const uint8_t* verify_key, size_t verify_key_len,
+                           const uint8_t* app_ctx, size_t ctx_len, int agg_id, const uint8_t* enc_agg_param, size_t agg_param_len, size_t n,
                            const uint8_t* nonces, const uint8_t* public_shares, const uint8_t* input_shares,
                            uint8_t* prep_shares_out, uint8_t* jr_seeds_out, uint8_t* out_shares_out,
                            int32_t* status_out);

@@ -101,3 +101,32 @@ def test_cache_not_used_across_different_inputs(mastic_amd):
     m.prep_init_device(dev, vk, CTX, 1, (1, p1, False))  # other aggregator
     assert not m.last_prep_was_cached()
     m.set_frontier_cache(False)
+
+
+def test_cache_miss_when_counts_match_but_paths_differ(mastic_amd):
+    """The hit rule compares level L-1's node paths, not just the per-level
+    node counts: a level-2 call whose parents hang off the other level-0 node
+    (same counts 1, 1, 1 as the cached level-1 tree) must evaluate the whole
+    tree, and its results must equal a cache-off context's."""
+    rng = random.Random(79)
+    m = mastic_amd.MasticCount(5)
+    ref = mastic_amd.MasticCount(5)
+    (alphas, weights, nonces, rands) = _reports(m, rng, 70, 6)
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    dev = m.reports_upload(nonces, pub, in0, in1)
+    dev_ref = ref.reports_upload(nonces, pub, in0, in1)
+    m.set_frontier_cache(True)
+    vk = bytes(range(16))
+    lvl1 = (1, ((False, False), (False, True)), False)              # tree under 0
+    lvl2 = (2, ((True, False, False), (True, False, True)), False)  # tree under 1: counts 1, 1, 1
+    assert m.tree_stats(lvl1)[0] == 4 and m.tree_stats(lvl2)[0] == 6
+    m.prep_init_device(dev, vk, CTX, 0, (0, ((False,), (True,)), False))
+    m.prep_init_device(dev, vk, CTX, 0, lvl1)
+    assert m.last_prep_was_cached()
+    m.prep_init_device(dev, vk, CTX, 0, lvl2)
+    assert not m.last_prep_was_cached()
+    got = m.prep_result(dev, 0, lvl2, want_out_shares=True)
+    ref.prep_init_device(dev_ref, vk, CTX, 0, lvl2)
+    want = ref.prep_result(dev_ref, 0, lvl2, want_out_shares=True)
+    assert got[0] == want[0] and got[2] == want[2]
+    m.set_frontier_cache(False)

@@ -227,6 +227,30 @@ def test_long_context_string(mastic_amd):
     _check_against_oracle(m, o, ctx, vk, ap, alphas, weights, nonces, rands)
 
 
+@pytest.mark.parametrize("vk_len", [16, 17, 0, 255])
+def test_verify_key_lengths(mastic_amd, vk_len):
+    """The verify key is XofTurboShake128's length-prefixed seed
+    (mastic.py:302-306,499-510): the reference driver passes 16 bytes
+    (examples.py:38,176).  Eval proofs and query randomness (FLP verifier
+    shares of a Sum circuit) must match the oracle for any length."""
+    rng = random.Random(40 + vk_len)
+    m = mastic_amd.MasticSum(5, 13)
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 3)
+    vk = bytes(rng.getrandbits(8) for _ in range(vk_len))
+    for (level, nprefix, wc) in [(0, 2, True), (4, 5, False)]:
+        ap = _random_agg_param(m, rng, alphas, level, nprefix, wc)
+        _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=False)
+
+
+def test_verify_key_too_long_rejected(mastic_amd):
+    m = mastic_amd.MasticCount(3)
+    ap = (0, ((False,), (True,)), True)
+    with pytest.raises(ValueError):
+        m.prep_init_batch(bytes(256), CTX, 0, ap, bytes(16), bytes(m.public_share_size()),
+                          bytes(m.input_share_size(0)))
+
+
 def test_empty_ctx_and_single_prefix(mastic_amd):
     rng = random.Random(8)
     m = mastic_amd.MasticCount(3)

@@ -66,7 +66,7 @@ def test_example_attribute_based_metrics_mode():
     bits = 8
     ctx = b'example_attribute_based_metrics_mode'
     mastic = MasticSum(bits, 3)
-    verify_key = os.urandom(32)
+    verify_key = os.urandom(16)  # gen_rand(16), as examples.py:176
 
     def h(attr):
         return mastic.vidpf.test_index_from_int(hashlib.sha3_256(attr.encode('ascii')).digest()[0], bits)
@@ -143,3 +143,51 @@ def test_sweep_drops_tampered_report():
     assert all(t.n_valid == 6 for t in trace[2:] if t.prefixes)
     assert hh == []  # 101101 falls to 3 copies
     assert np.all(np.array([t.n_valid for t in trace]) <= 7)
+
+
+class _TotalAtLeast:
+    """Threshold on a vector-valued aggregate (Histogram): its total."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __le__(self, other):  # `count >= threshold` with count a list
+        return sum(other) >= self.t
+
+
+def test_sweep_joint_rand_confirmation_drops_report():
+    """prep_next's joint-rand confirmation (mastic.py:364-377, examples.py:67):
+    a report whose leader input share carries a corrupted peer joint-rand part
+    (mastic.py:516-529) derives a joint-rand seed that differs from the prep
+    message; the batched check flags exactly that report and the sweep drops
+    it from every level."""
+    from mastic_amd import MasticHistogram
+    from mastic_amd.heavy_hitters import compute_heavy_hitters, joint_rand_confirmed
+    bits = 4
+    mastic = MasticHistogram(bits, 4, 2)
+    assert mastic.JOINT_RAND_LEN > 0
+    ctx = b'jr'
+    rng = random.Random(13)
+    meas = [(index(0b1011, bits), 2)] * 5 + [(index(0b0100, bits), 1)] * 4
+    reports = _reports(mastic, ctx, meas, rng)
+    (nonce, pub, ins) = reports[0]
+    (key, proof_share, seed, peer) = ins[0]
+    ins = [(key, proof_share, seed, bytes([peer[0] ^ 0x80]) + peer[1:]), ins[1]]
+    reports[0] = (nonce, pub, ins)
+    # the batched pieces directly: the confirmation fails for report 0 only
+    from mastic_amd.heavy_hitters import _encode_reports
+    dev = mastic.reports_upload(*_encode_reports(mastic, reports))
+    vk = rng.randbytes(16)
+    ap = (0, ((False,), (True,)), True)
+    enc = mastic.encode_agg_param(ap)
+    sh = []
+    for a in range(2):
+        mastic.prep_init_device(dev, vk, ctx, a, enc)
+        sh.append(mastic.prep_result(dev, a, enc))
+    (msgs, _valid) = mastic.decide_batch(ctx, enc, sh[0][0], sh[1][0])
+    ok = joint_rand_confirmed(msgs, sh[0][1], sh[1][1], len(meas))
+    assert list(ok) == [False] + [True] * (len(meas) - 1)
+    trace = []
+    hh = compute_heavy_hitters(mastic, ctx, {'default': _TotalAtLeast(4)}, dev, verify_key=vk, trace=trace)
+    assert all(t.n_valid == len(meas) - 1 for t in trace if t.prefixes)
+    assert hh == [index(0b0100, bits), index(0b1011, bits)]

@@ -51,6 +51,8 @@ class _StubMastic:
     aggregator 0 and zeros for aggregator 1; ``bad`` reports fail decide from
     level ``bad_level`` on."""
     VERIFY_KEY_SIZE = 32
+    OUTPUT_LEN = 0
+    JOINT_RAND_LEN = 0
 
     def __init__(self, bits, bad=(), bad_level=0):
         class V:
@@ -155,3 +157,17 @@ def test_child_packing_matches_pack_path():
         prefix = tuple(bool(rng.getrandbits(1)) for _ in range(length))
         for bit in (False, True):
             assert _child_packed(_pack_path(prefix), length, bit) == _pack_path(prefix + (bit,))
+
+
+def test_joint_rand_confirmation_mask():
+    """prep_next's check (mastic.py:369-375) for both aggregators, batched."""
+    from mastic_amd.heavy_hitters import joint_rand_confirmed
+    rng = random.Random(9)
+    n = 5
+    msgs = bytes(rng.getrandbits(8) for _ in range(32 * n))
+    j0 = bytearray(msgs)
+    j1 = bytearray(msgs)
+    j0[32 * 1 + 7] ^= 1      # report 1: leader's seed differs
+    j1[32 * 3 + 31] ^= 0x40  # report 3: helper's seed differs
+    assert list(joint_rand_confirmed(msgs, bytes(j0), bytes(j1), n)) == [True, False, True, False, True]
+    assert len(joint_rand_confirmed(b"", b"", b"", 0)) == 0
