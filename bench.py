@@ -52,10 +52,17 @@ CONFIGS = {
                          "128 random 16-bit strings, weights Bernoulli(0.9), threshold 10), both aggregators per "
                          "level: the reference's CPU-sized case"),
     "c3sweep": dict(circuit="Count", kw=dict(bits=256), prefixes=0, reports=65536, sweep=True, pool=2 ** 20, zipf=1.1,
-                    weight_p=1.0, threshold=None,
+                    weight_p=1.0, threshold=None, spec_sample=8192, spec_every=8,
                     desc="C3: Mastic(BITS=256, Count) weighted heavy hitters, full 256-level threshold-pruned "
                          "sweep (Zipf(1.1) over 2^20 random 256-bit strings, threshold 0.05% of all reports), "
                          "both aggregators per level; run with --steps 1 --warmup 0"),
+    "c2sweep": dict(circuit="Sum", kw=dict(bits=32, max_measurement=255), prefixes=0, reports=1000000, sweep=True,
+                    pool="c2", zipf=1.1, threshold_frac=0.0005, spec_sample=65536,
+                    desc="north_star: Mastic(BITS=32, Sum max=255) (C2's VDAF) weighted heavy hitters over 1M "
+                         "reports, full 32-level threshold-pruned sweep (alphas Zipf(1.1) over C2's 10k random "
+                         "32-bit attributes, weights uniform 0..255, threshold 0.05% of the expected total "
+                         "weight), both aggregators per level, weight check at level 0; run with --steps 1 "
+                         "--warmup 0"),
     "c4": dict(circuit="Histogram", kw=dict(bits=64, length=64, chunk_length=8), prefixes=1000, reports=12288,
                desc="C4: Mastic(BITS=64, Histogram length=64 chunk 8, Field128) prep_init+aggregate, level 63"),
     "c5": dict(circuit="SumVec", kw=dict(bits=32, length=1024, sum_vec_bits=1, chunk_length=32), prefixes=100,
@@ -193,20 +200,39 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
-    pool = np.random.default_rng(seed).integers(0, 256, size=(cfg["pool"], bits // 8), dtype=np.uint8)
+    if cfg.get("pool") == "c2":  # the C2 attribute set (same draws as bench --config c2)
+        pool = _attrs(np.random.default_rng(seed), bits, 10000)
+    else:
+        pool = np.random.default_rng(seed).integers(0, 256, size=(cfg["pool"], bits // 8), dtype=np.uint8)
     rrng = np.random.default_rng(seed * 1000003 + rank)
     ranks = rrng.zipf(cfg["zipf"], size=n_rep)
     while (ranks > len(pool)).any():
         bad = ranks > len(pool)
         ranks[bad] = rrng.zipf(cfg["zipf"], size=int(bad.sum()))
     alpha_b = pool[ranks - 1].tobytes()
-    betas = (rrng.random(n_rep) < cfg["weight_p"]).astype("<u8").tobytes()
+    if cfg["circuit"] == "Sum":  # weights uniform 0..max
+        w = rrng.integers(0, kw["max_measurement"] + 1, size=n_rep)
+        nb = int(kw["max_measurement"]).bit_length()
+        off = 2 ** nb - 1 - kw["max_measurement"]
+        betas = np.concatenate([(w[:, None] >> np.arange(nb)) & 1, ((w + off)[:, None] >> np.arange(nb)) & 1],
+                               axis=1).astype("<u8").tobytes()
+        # 0.05 % of the job's expected total weight (identical on every rank)
+        threshold = max(1, int(np.ceil(cfg["threshold_frac"] * n_rep * world * kw["max_measurement"] / 2)))
+    else:
+        w = (rrng.random(n_rep) < cfg["weight_p"]).astype(np.int64)
+        threshold = cfg["threshold"] or max(1, int(np.ceil(0.0005 * n_rep * world)))
+        betas = w.astype("<u8").tobytes()
     nonces = rrng.integers(0, 256, size=16 * n_rep, dtype=np.uint8).tobytes()
     rands = rrng.integers(0, 256, size=m.RAND_SIZE * n_rep, dtype=np.uint8).tobytes()
     reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
-    vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
-    thresholds = {"default": cfg["threshold"] or max(1, int(np.ceil(0.0005 * n_rep * world)))}
+    del betas, nonces, rands
+    vk = np.random.default_rng(0x4D41).integers(0, 256, size=16, dtype=np.uint8).tobytes()  # gen_rand(16)
+    thresholds = {"default": threshold}
     merge = merge_field_shares(m, dist) if dist else None
+    if cfg.get("memory_budget_gb"):
+        import ctypes
+        from mastic_amd import _lib
+        _lib.lib().mastic_set_memory_budget(m._ctx, ctypes.c_uint64(int(cfg["memory_budget_gb"] * 2 ** 30)))
 
     cached_levels = []
 
@@ -240,6 +266,33 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
         dt = float(tt.item())
 
     units = sum(2 * n_rep * len(lv.prefixes) for tr in traces for lv in tr) * world
+    # plaintext check (single rank): the heavy hitters are exactly the
+    # attributes whose total weight reaches the threshold (every prefix of one
+    # has at least its weight), and sampled levels' aggregates equal the
+    # plaintext prefix sums (talks/func.py:49-80)
+    plain_ok = None
+    if world == 1:
+        ab = (bits + 7) // 8
+        arr = np.frombuffer(alpha_b, np.uint8).reshape(-1, ab)
+        keys, inv = np.unique(arr, axis=0, return_inverse=True)
+        tot = np.bincount(inv.ravel(), weights=w)
+        want = set(bytes(k) for (k, t) in zip(keys, tot) if t >= threshold)
+        got = set(np.packbits(np.array(p, dtype=bool)).tobytes() for p in hh)
+        plain_ok = got == want
+        for lv in traces[0][::max(1, len(traces[0]) // 6)]:
+            if not lv.prefixes or lv.level >= 63:
+                continue
+            L = lv.level + 1
+            val = np.zeros(len(arr), dtype=np.uint64)
+            for j in range((L + 7) // 8):
+                val = (val << np.uint64(8)) | arr[:, j].astype(np.uint64)
+            val >>= np.uint64(8 * ((L + 7) // 8) - L)
+            sums = {}
+            u, iv = np.unique(val, return_inverse=True)
+            for (k, t) in zip(u.tolist(), np.bincount(iv.ravel(), weights=w).tolist()):
+                sums[k] = int(t)
+            pv = [int("".join("1" if b else "0" for b in p), 2) for p in lv.prefixes]
+            plain_ok = plain_ok and [sums.get(x, 0) for x in pv] == list(lv.agg_result)
     # node evaluations actually performed: a level served from the frontier cache evaluates
     # only its new tree level (both children of every distinct length-L prefix)
     hit = set(cached_levels)
@@ -279,6 +332,7 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "max_candidates_per_level": max(widths),
             "sum_candidates_over_levels": sum(widths),
             "heavy_hitters": len(hh),
+            "heavy_hitters_equal_plaintext": plain_ok,
             "frontier_cache": bool(args.frontier_cache),
             "levels_evaluated_from_cache": len(cached_levels),
             "node_evals_per_step": nodes // args.steps,
@@ -305,6 +359,44 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "prep_init_total": sum(t[6] for t in timing) / args.steps,
         },
     }
+    out["rates"] = {
+        "with_frontier_cache" if args.frontier_cache else "spec_literal": units / dt,
+        "unit": "report*prefix/s (both aggregators' prep_init + decide + fold per level, whole sweep)",
+    }
+    if args.frontier_cache and cfg.get("spec_sample"):
+        # spec-literal rate: every level's prep_init evaluates
+        # its whole tree, as the reference does; the same per-level body on a
+        # bounded sample of the reports with the timed sweep's candidate lists
+        m.set_frontier_cache(False)
+        ns = min(cfg["spec_sample"], n_rep)
+        sample = reps.view(0, ns)
+        lvls = [lv for lv in traces[0] if lv.prefixes][::cfg.get("spec_every", 1)]
+        m.synchronize()
+        if dist:
+            dist.barrier()
+        t2 = time.perf_counter()
+        su = 0
+        for lv in lvls:
+            enc = m.encode_agg_param((lv.level, tuple(lv.prefixes), lv.level == 0))
+            for agg_id in range(2):
+                m.prep_init_device(sample, vk, ctx, agg_id, enc)
+            sh = [m.prep_result(sample, agg_id, enc) for agg_id in range(2)]
+            (_msgs, valid) = m.decide_batch(ctx, enc, sh[0][0], sh[1][0])
+            for agg_id in range(2):
+                m.aggregate_device(agg_id, enc, valid == 1, raw=True)
+            su += 2 * ns * len(lv.prefixes)
+        m.synchronize()
+        if dist:
+            dist.barrier()
+        t_spec = time.perf_counter() - t2
+        if dist:
+            tt = torch.tensor([t_spec], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_spec = float(tt.item())
+        out["rates"]["spec_literal_sampled"] = su * world / t_spec
+        out["rates"]["spec_literal_sample"] = "%d reports per rank, %d of the sweep's levels (every %d-th), its " \
+            "candidate lists, frontier cache off: each level evaluates its whole tree" % (
+                ns, len(lvls), cfg.get("spec_every", 1))
     if rank == 0 and world == 1 and args.cpu_baseline:
         # oracle prep_init (leader) of one report per process at 8 levels spread over the sweep,
         # with the GPU trace's candidate prefixes: a bounded sample of the same workload

@@ -495,6 +495,7 @@ struct AesArgs {
     // fr_w_in indexed by the parent's node index (parent_node) instead of its ordinal
     uint32_t* last_w;
     int wp_by_node;
+    int in_stride;  // plane stride of cs_in / fr_w_in (the cache's, on a hit; else the work buffer's)
     // node proofs of the PREVIOUS level (vidpf.py:366-380, :321-323), computed
     // by the workgroup's EVAL_PROOF_WAVES proof waves beside the AES waves
     int pv_level;                   // level - 1
@@ -556,6 +557,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     aes_perm_fill(T, threadIdx.x, 64 * EVAL_WAVES);
 
     const int S = pl.stride;
+    const int S_in = FC ? a.in_stride : S;  // cs_in / fr_w_in
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = blockIdx.x * 64 + lane;
@@ -588,8 +590,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         for (int node = nbeg; node < nend; node++) {
             uint32_t sd[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_in + ((size_t)node * 5 + i) * S, lb);
-            const uint32_t t = pld(a.cs_in + ((size_t)node * 5 + 4) * S, lb);
+            for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_in + ((size_t)node * 5 + i) * S_in, lb);
+            const uint32_t t = pld(a.cs_in + ((size_t)node * 5 + 4) * S_in, lb);
             node_proof_one(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
                            [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
         }
@@ -637,8 +639,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         } else {
             const int pn = a.parent_node[pi];
 #pragma unroll
-            for (int i = 0; i < 4; i++) ps[i] = pld(a.cs_in + ((size_t)pn * 5 + i) * S, lb);
-            pctrl = pld(a.cs_in + ((size_t)pn * 5 + 4) * S, lb);
+            for (int i = 0; i < 4; i++) ps[i] = pld(a.cs_in + ((size_t)pn * 5 + i) * S_in, lb);
+            pctrl = pld(a.cs_in + ((size_t)pn * 5 + 4) * S_in, lb);
         }
     };
     uint32_t nps[4], npctrl;
@@ -738,7 +740,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
         int wpi = pi;
         if constexpr (FC) wpi = a.wp_by_node ? a.parent_node[pi] : pi;
-        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, wpi * vl + e, S, r) : F::zero(); };
+        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, wpi * vl + e, S_in, r) : F::zero(); };
         int e_fast = 0;  // elements completed by the fast path
         if constexpr (!QUAD) {
             // Fast path: block b (counter b + 1) of each child's convert stream

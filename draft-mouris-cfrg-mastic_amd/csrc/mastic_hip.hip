@@ -86,19 +86,34 @@ inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 // cached message is a prefix of the next one), the last level's child seeds /
 // control bits and payloads, and the root sum; a call whose tree extends the
 // cached one by one level evaluates and absorbs only that level.
+// Planes of all n reports (stride S, independent of the HBM-budget chunks a
+// call runs in, so a sweep's chunking may change from level to level); one
+// slot per aggregator: a hit reads its parents from the slot before the same
+// chunk's new level is copied over them (stream order), and a slot that must
+// grow is replaced by a larger one whose predecessor is retired only after
+// the call (mastic_ctx::graveyard).
 struct LevelCache {
     bool valid = false;
     uint64_t rep_gen = 0;
     size_t n = 0;
-    int stride = 0;
-    std::vector<uint8_t> key;                   // verify key || ctx
+    size_t S = 0;                               // plane stride (n rounded up to 64, plus padding)
+    std::vector<uint8_t> key;                   // u8(len) || verify key || ctx
     int L = -1;                                 // level of the cached call
     std::vector<int> n_parents;                 // per level 0..L
     std::vector<uint32_t> paths;                // child paths of level L (8 words per node)
-    DevBuf sp;                                  // both binder sponges after levels 0..L (2 x 50 planes)
-    DevBuf cs[2], w[2], rootsum;                // last level's seeds/ctrl and payloads; root sum
-    int wcur = 0;                               // which cs / w hold the cached level (the other is written)
+    DevBuf sp, rootsum;                         // both binder sponges (2 x 50 planes); root sum (wl planes)
+    DevBuf cs, w;                               // last level: seeds / ctrl [node][5], payloads [node][wl]
+    size_t nodes_cap = 0;                       // nodes cs / w can hold
     void drop() { valid = false; }
+    void release() {
+        drop();
+        sp.release();
+        rootsum.release();
+        cs.release();
+        w.release();
+        nodes_cap = 0;
+        S = 0;
+    }
 };
 
 }  // namespace
@@ -150,6 +165,11 @@ struct mastic_ctx {
     bool frontier_cache = false;  // mastic_set_frontier_cache
     bool last_hit = false;        // the last prep_init evaluated only its last level
     LevelCache lc[2];
+    std::vector<void*> graveyard;  // replaced cache slots, freed once the streams are idle
+    void bury() {
+        for (void* q : graveyard) (void)hipFree(q);
+        graveyard.clear();
+    }
     // timing
     // timing events and results of the last prep_init of each aggregator
     // (both may be queued before either's results are fetched)
@@ -160,6 +180,7 @@ struct mastic_ctx {
     } tm[2];
     int tcur = 0;  // aggregator whose timing mastic_last_timing* report (last prep_init / prep_result)
     ~mastic_ctx() {
+        bury();
         for (auto& kv : trees) delete kv.second;
         for (auto& x : tm)
             for (auto e : x.ev) (void)hipEventDestroy(e);
@@ -479,11 +500,13 @@ struct WorkLayout {
     size_t words = 0;  // per report (plane count)
     size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
         rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, cs[2], fr_w[2], onehot[3],
-        payload[3], out;
+        payload[3], out, lastw;
 };
 static constexpr int NSLOT = 3;  // level buffers in flight between eval and absorb
 
-static WorkLayout work_layout(const McParams& p, const Tree* t) {
+// cache: the frontier cache is on (the last level's payloads of every node
+// are staged in the work buffer before they are copied into the cache)
+static WorkLayout work_layout(const McParams& p, const Tree* t, bool cache = false) {
     WorkLayout w;
     size_t o = 0;
     auto take = [&](size_t n) {
@@ -524,6 +547,7 @@ static WorkLayout work_layout(const McParams& p, const Tree* t) {
         w.payload[k] = take((size_t)t->max_parents * wl);
     }
     w.out = take((size_t)std::max(t->n_prefixes, 1) * (1 + p.output_len) * p.w32);
+    w.lastw = take(cache ? (size_t)2 * t->n_parents[t->L] * wl : 0);
     w.words = o;
     return w;
 }
@@ -616,9 +640,13 @@ static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst
     return 0;
 }
 
+// One chunk of reports [base, base + n) of a prep_init.  lc: the frontier
+// cache (or null); on a hit the parents' seeds / payloads are read from
+// cin_cs / cin_w (the cache slot, or its predecessor when the slot grew).
 template <class F>
 static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
-                     size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit) {
+                     size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit, const uint32_t* cin_cs,
+                     const uint32_t* cin_w) {
     const McParams& p = c->p;
     uint32_t* W = c->work.as<uint32_t>();
     Planes pl = make_planes(W, wl, n, stride);
@@ -694,15 +722,24 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
         return 0;
     };
+    // cache planes <-> work planes of this chunk (columns base .. base + n)
+    auto from_cache = [&](uint32_t* dst, const uint32_t* src, size_t planes) -> int {
+        HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)stride * 4, src + base, lc->S * 4, (size_t)n * 4, planes,
+                                   hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    };
+    auto to_cache = [&](uint32_t* dst, const uint32_t* src, size_t planes) -> int {
+        HIPCHK(c, hipMemcpy2DAsync(dst + base, lc->S * 4, src, (size_t)stride * 4, (size_t)n * 4, planes,
+                                   hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    };
     if (hit) {
         // levels 0..L-1 from the cache.  The binder messages are BFS-ordered
         // (mastic.py:263-275), so the cached call's message is a prefix of
         // this one's: both sponges resume from their states at the end of the
         // cached call (mid-block, unpadded; k_finalize pads a register copy).
-        HIPCHK(c, hipMemcpyAsync(pl.sp_onehot, lc->sp.p, (size_t)50 * stride * 4, hipMemcpyDeviceToDevice,
-                                 c->stream));
-        HIPCHK(c, hipMemcpyAsync(pl.sp_payload, lc->sp.as<uint32_t>() + (size_t)50 * stride,
-                                 (size_t)50 * stride * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (from_cache(pl.sp_onehot, lc->sp.as<uint32_t>(), 50)) return -1;
+        if (from_cache(pl.sp_payload, lc->sp.as<uint32_t>() + (size_t)50 * lc->S, 50)) return -1;
         // (no timing events for the cached levels: nothing is launched for
         // them, and 6 records per level cost ~1.4 ms of host time at L = 255)
         for (int lv = 0; lv < t->L; lv++) {
@@ -710,8 +747,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             f_pl = (f_pl + (lv > 0 ? t->n_parents[lv] * wlw * 4 : 0)) % KECCAK_RATE;
         }
         // the root sum of the cached level-0 evaluation (counter check)
-        HIPCHK(c, hipMemcpyAsync(pl.rootsum, lc->rootsum.p, (size_t)wlw * stride * 4, hipMemcpyDeviceToDevice,
-                                 c->stream));
+        if (from_cache(pl.rootsum, lc->rootsum.as<uint32_t>(), (size_t)wlw)) return -1;
     }
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
@@ -724,14 +760,15 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
-        a.cs_in = hit ? lc->cs[lc->wcur].as<uint32_t>() : plane(wl.cs[(l + 1) & 1]);
+        a.cs_in = hit ? cin_cs + base : plane(wl.cs[(l + 1) & 1]);
         a.cs_out = plane(wl.cs[l & 1]);
-        a.fr_w_in = hit ? lc->w[lc->wcur].as<uint32_t>() : plane(wl.fr_w[(l + 1) & 1]);
+        a.fr_w_in = hit ? cin_w + base : plane(wl.fr_w[(l + 1) & 1]);
+        a.in_stride = hit ? (int)lc->S : stride;
         a.fr_w_out = plane(wl.fr_w[l & 1]);
         a.payload = pay_buf(l);
         a.out = plane(wl.out);
         a.force_slow_blk = c->force_slow_blk;
-        a.last_w = (lc && l == t->L) ? lc->w[lc->wcur ^ 1].as<uint32_t>() : nullptr;
+        a.last_w = (lc && l == t->L) ? plane(wl.lastw) : nullptr;
         a.wp_by_node = hit ? 1 : 0;
         a.aes_waves = EVAL_WAVES - c->proof_waves;
         a.proof_prio = c->proof_prio;
@@ -814,19 +851,15 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     }
     HIPCHK(c, hipGetLastError());
     if (lc) {
-        // frontier cache for the next level: last level's seeds/ctrl and payloads, root sum
+        // frontier cache for the next level: last level's seeds/ctrl and payloads, root sum.
+        // Stream order: this chunk's level kernel has read its parents from the slot.
         const size_t nl = (size_t)2 * t->n_parents[t->L];
-        HIPCHK(c, hipMemcpyAsync(lc->cs[lc->wcur ^ 1].p, plane(wl.cs[t->L & 1]), nl * 5 * stride * 4,
-                                 hipMemcpyDeviceToDevice, c->stream));
-        if (!hit)
-            HIPCHK(c, hipMemcpyAsync(lc->rootsum.p, pl.rootsum, (size_t)wlw * stride * 4, hipMemcpyDeviceToDevice,
-                                     c->stream));
+        if (to_cache(lc->cs.as<uint32_t>(), plane(wl.cs[t->L & 1]), nl * 5)) return -1;
+        if (to_cache(lc->w.as<uint32_t>(), plane(wl.lastw), nl * wlw)) return -1;
+        if (!hit && to_cache(lc->rootsum.as<uint32_t>(), pl.rootsum, (size_t)wlw)) return -1;
         // both sponges after levels 0..L (stream waited for abs_done[L] above)
-        HIPCHK(c, hipMemcpyAsync(lc->sp.p, pl.sp_onehot, (size_t)50 * stride * 4, hipMemcpyDeviceToDevice,
-                                 c->stream));
-        HIPCHK(c, hipMemcpyAsync(lc->sp.as<uint32_t>() + (size_t)50 * stride, pl.sp_payload,
-                                 (size_t)50 * stride * 4, hipMemcpyDeviceToDevice, c->stream));
-        lc->wcur ^= 1;
+        if (to_cache(lc->sp.as<uint32_t>(), pl.sp_onehot, 50)) return -1;
+        if (to_cache(lc->sp.as<uint32_t>() + (size_t)50 * lc->S, pl.sp_payload, 50)) return -1;
     }
     // results -> the agg_id slot (plane stride = all reports)
     Result& R = c->res[agg_id];
@@ -891,30 +924,21 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         R.ready = true;
         return 0;
     }
-    const uint64_t budget = default_budget(c);
-    const size_t per_report = wl.words * 4;
-    // Plane rows are padded by stride_pad words: with a power-of-two row
-    // length every word of a report sits at the same address bits modulo a
-    // large power of two, and the 42-plane block loads of the binder sponges
-    // all land on the same memory channels.
     const size_t pad = (size_t)c->stride_pad;
-    size_t by_budget = (budget / per_report) / 64 * 64;
-    if (by_budget > pad + 64) by_budget -= pad;  // the padded rows count against the budget too
-    size_t chunk = std::min<size_t>(round_up(n, 64), by_budget);
-    if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
-    if (!c->work.ensure(per_report * (chunk + pad)))
-        return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * (chunk + pad));
-    // frontier cache (one-chunk batches with tiled binder buffers only)
+    // frontier cache (tiled binder buffers only): decide hit / miss and size
+    // the slot before the work buffer, so the HBM budget sees the cache
     LevelCache* lc = nullptr;
     bool hit = false;
+    const uint32_t *cin_cs = nullptr, *cin_w = nullptr;
+    std::vector<void*> retire_after;  // slot buffers the hit still reads
     std::vector<uint8_t> lkey(1, (uint8_t)vk_len);
     lkey.insert(lkey.end(), verify_key, verify_key + vk_len);
     lkey.insert(lkey.end(), app_ctx, app_ctx + ctx_len);
-    if (c->frontier_cache && c->binder_tiled && chunk >= n) {
+    if (c->frontier_cache && c->binder_tiled) {
         lc = &c->lc[agg_id];
-        const int stride1 = (int)(round_up(n, 64) + pad);
+        const size_t S1 = round_up(n, 64) + pad;
         const int L = t->L;
-        hit = lc->valid && lc->rep_gen == rep->gen && lc->n == n && lc->stride == stride1 && lc->key == lkey &&
+        hit = lc->valid && lc->rep_gen == rep->gen && lc->n == n && lc->S == S1 && lc->key == lkey &&
               !t->weight_check && L == lc->L + 1 && (size_t)L <= lc->n_parents.size() &&
               std::equal(t->n_parents.begin(), t->n_parents.begin() + L, lc->n_parents.begin()) &&
               // level L-1's node paths fix every level above (each level's
@@ -922,40 +946,91 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
               // they and the node counts decide that the trees agree there
               lc->paths.size() == (t->off[L] - t->off[L - 1]) * 8 &&
               std::equal(lc->paths.begin(), lc->paths.end(), t->child_path.begin() + t->off[L - 1] * 8);
-        // tiles for every 64-row group of the padded stride: the sponge
-        // kernels run over all pl.stride rows, padding included
-        const size_t S1 = (size_t)stride1, groups = S1 / 64;
+        auto retire = [&](DevBuf& b) {  // queued kernels may still read it
+            if (b.p && b.own) c->graveyard.push_back(b.p);
+            b.p = nullptr;
+            b.bytes = 0;
+        };
+        if (lc->S != S1) {
+            retire(lc->sp);
+            retire(lc->rootsum);
+            retire(lc->cs);
+            retire(lc->w);
+            lc->nodes_cap = 0;
+            lc->S = S1;
+        }
         const size_t wlw = (size_t)p.value_len * p.w32;
-        (void)groups;
         const size_t nl = (size_t)2 * t->n_parents[L];
-        const bool ok = lc->sp.ensure(100 * S1 * 4) && lc->cs[lc->wcur ^ 1].ensure(nl * 5 * S1 * 4) &&
-                        lc->w[lc->wcur ^ 1].ensure(nl * wlw * S1 * 4) && lc->rootsum.ensure(wlw * S1 * 4);
+        bool ok = lc->sp.ensure(100 * S1 * 4) && lc->rootsum.ensure(wlw * S1 * 4);
+        if (ok && nl > lc->nodes_cap) {
+            // grow geometrically (a sweep's frontier widens over several levels)
+            const size_t cap = std::max(nl, lc->nodes_cap + lc->nodes_cap / 4);
+            DevBuf ncs, nw;
+            ok = ncs.ensure(cap * 5 * S1 * 4) && nw.ensure(cap * wlw * S1 * 4);
+            if (ok) {
+                if (hit) {
+                    cin_cs = lc->cs.as<uint32_t>();
+                    cin_w = lc->w.as<uint32_t>();
+                    retire_after = {lc->cs.p, lc->w.p};
+                    lc->cs.p = lc->w.p = nullptr;
+                    lc->cs.bytes = lc->w.bytes = 0;
+                } else {
+                    retire(lc->cs);
+                    retire(lc->w);
+                }
+                std::swap(lc->cs.p, ncs.p);
+                std::swap(lc->cs.bytes, ncs.bytes);
+                std::swap(lc->w.p, nw.p);
+                std::swap(lc->w.bytes, nw.bytes);
+                lc->nodes_cap = cap;
+            }
+        }
         if (!ok) {  // not enough HBM for the cache: evaluate without it
-            lc->drop();
+            for (void* q : retire_after) c->graveyard.push_back(q);
+            retire_after.clear();
+            lc->release();
             lc = nullptr;
             hit = false;
+        } else if (hit && !cin_cs) {
+            cin_cs = lc->cs.as<uint32_t>();
+            cin_w = lc->w.as<uint32_t>();
         }
+        if (!hit && lc) lc->drop();  // refilled by this call
     } else {
         c->lc[agg_id].drop();
     }
+    if (lc) wl = work_layout(p, t, true);
+    const uint64_t budget = default_budget(c);
+    const size_t per_report = wl.words * 4;
+    // Plane rows are padded by stride_pad words: with a power-of-two row
+    // length every word of a report sits at the same address bits modulo a
+    // large power of two, and the 42-plane block loads of the binder sponges
+    // all land on the same memory channels.
+    size_t by_budget = (budget / per_report) / 64 * 64;
+    if (by_budget > pad + 64) by_budget -= pad;  // the padded rows count against the budget too
+    size_t chunk = std::min<size_t>(round_up(n, 64), by_budget);
+    if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
+    if (!c->work.ensure(per_report * (chunk + pad)))
+        return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * (chunk + pad));
     size_t evi = 0;
     hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
     HIPCHK(c, hipEventRecord(t0, c->stream));
     for (size_t b = 0; b < n; b += chunk) {
         const int nn = (int)std::min(chunk, n - b);
         const int stride = (int)(round_up(nn, 64) + pad);
-        rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit)
-                           : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit);
+        rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w)
+                           : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w);
         if (rc) {
+            for (void* q : retire_after) c->graveyard.push_back(q);
             if (lc) lc->drop();
             return rc;
         }
     }
+    for (void* q : retire_after) c->graveyard.push_back(q);
     if (lc) {
         lc->valid = true;
         lc->rep_gen = rep->gen;
         lc->n = n;
-        lc->stride = (int)(round_up(n, 64) + pad);
         lc->key = lkey;
         lc->L = t->L;
         lc->n_parents.assign(t->n_parents.begin(), t->n_parents.begin() + t->L + 1);
@@ -995,6 +1070,7 @@ extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_share
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
     c->tcur = agg_id;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bury();  // the stream is idle (it joined the sponge stream before k_finalize)
     const McParams& p = c->p;
     const size_t n = R.n, S = R.stride;
     if (n == 0) return 0;
@@ -1151,6 +1227,7 @@ extern "C" int mastic_synchronize(mastic_ctx* c) {
     DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bury();
     return 0;
 }
 
@@ -1549,16 +1626,10 @@ extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamSynchronize(c->stream2);
         }
-        if (!on)
-            for (auto& x : c->lc) {
-                x.drop();
-                x.sp.release();
-                x.cs[0].release();
-                x.cs[1].release();
-                x.w[0].release();
-                x.w[1].release();
-                x.rootsum.release();
-            }
+        if (!on) {
+            for (auto& x : c->lc) x.release();
+            c->bury();
+        }
     }
     if (last_hit) *last_hit = c->last_hit ? 1 : 0;
     return 0;

@@ -130,3 +130,46 @@ def test_cache_miss_when_counts_match_but_paths_differ(mastic_amd):
     want = ref.prep_result(dev_ref, 0, lvl2, want_out_shares=True)
     assert got[0] == want[0] and got[2] == want[2]
     m.set_frontier_cache(False)
+
+
+def test_cache_across_hbm_chunks(mastic_amd):
+    """The cache holds planes of all reports, independent of the HBM-budget
+    chunks a call runs in: with 64- or 128-report chunks (changing from level
+    to level) the cached levels still hit and every level is bit-identical to
+    a cache-off context's."""
+    import ctypes
+    from mastic_amd import _lib
+    from mastic_amd.heavy_hitters import compute_heavy_hitters
+    rng = random.Random(80)
+    m_off = mastic_amd.MasticSum(9, 5)
+    m_on = mastic_amd.MasticSum(9, 5)
+    n = 150
+    (alphas, weights, nonces, rands) = _reports(m_off, rng, n, 10)
+    (pub, in0, in1) = m_off.shard_batch(CTX, alphas, weights, nonces, rands)
+    vk = bytes(rng.getrandbits(8) for _ in range(16))
+    trace = []
+    dev_off = m_off.reports_upload(nonces, pub, in0, in1)
+    compute_heavy_hitters(m_off, CTX, {"default": 3}, dev_off, verify_key=vk, trace=trace)
+    dev_on = m_on.reports_upload(nonces, pub, in0, in1)
+    m_on.set_frontier_cache(True)
+    hits = 0
+    try:
+        for lv in trace:
+            if not lv.prefixes:
+                break
+            ap = (lv.level, tuple(lv.prefixes), lv.level == 0)
+            enc = m_on.encode_agg_param(ap)
+            per = m_on.work_bytes(enc) + 64 * 1024  # + the cache's staging planes
+            groups = 1 if lv.level % 2 else 2        # 64- or 128-report chunks
+            _lib.lib().mastic_set_memory_budget(m_on._ctx, ctypes.c_uint64(per * 64 * groups + per * 64))
+            for agg_id in range(2):
+                m_off.prep_init_device(dev_off, vk, CTX, agg_id, ap)
+                m_on.prep_init_device(dev_on, vk, CTX, agg_id, ap)
+                hits += m_on.last_prep_was_cached()
+                a = m_off.prep_result(dev_off, agg_id, ap, want_out_shares=True)
+                b = m_on.prep_result(dev_on, agg_id, ap, want_out_shares=True)
+                assert a[0] == b[0] and a[2] == b[2], "level %d agg %d" % (lv.level, agg_id)
+    finally:
+        _lib.lib().mastic_set_memory_budget(m_on._ctx, ctypes.c_uint64(0))
+        m_on.set_frontier_cache(False)
+    assert hits >= 4, hits
