@@ -44,6 +44,7 @@ struct DevBuf {
         if (want == 0) want = 16;
         if (hipMalloc(&p, want) != hipSuccess) {
             p = nullptr;
+            (void)hipGetLastError();  // callers handle it; keep it out of later launch checks
             return false;
         }
         bytes = want;
@@ -650,14 +651,19 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const McParams& p = c->p;
     uint32_t* W = c->work.as<uint32_t>();
     Planes pl = make_planes(W, wl, n, stride);
-    // A frontier-cache hit writes every plane it reads (level L's correction
-    // words, keys, sponge states, seeds / payloads from the cache, ring slots,
-    // outputs) except the status plane: clear just that instead of the whole
-    // work buffer (~0.8 ms per call at C3 65,536 reports).
+    // Every level plane (child seeds, frontier payloads, proof / payload-
+    // difference ring, out shares, staged last-level payloads) is written
+    // before it is read: level l reads only level l-1's nodes / expanded
+    // nodes, which level l-1 wrote, and each candidate prefix is one child of
+    // level L.  So only the per-report header planes (keys, correction words,
+    // sponge states, FLP planes, status) are cleared -- 8 KB per report at C2
+    // instead of the whole 9.7 MB work area (119 GB of fill per C2 step).  A
+    // frontier-cache hit writes every header plane it reads except the
+    // status plane: it clears just that.
     if (hit)
         HIPCHK(c, hipMemsetAsync(pl.status, 0, (size_t)stride * 4, c->stream));
     else
-        HIPCHK(c, hipMemsetAsync(W, 0, wl.words * (size_t)stride * 4, c->stream));
+        HIPCHK(c, hipMemsetAsync(W, 0, wl.cs[0] * (size_t)stride * 4, c->stream));
     const size_t ps = mc_public_share_size(p), is = mc_input_share_size(p, agg_id);
     const uint8_t* ins = agg_id == 0 ? rep->in0.as<uint8_t>() : rep->in1.as<uint8_t>();
     const PrefixState* pfx = (const PrefixState*)c->pfx.p;
@@ -961,12 +967,24 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         }
         const size_t wlw = (size_t)p.value_len * p.w32;
         const size_t nl = (size_t)2 * t->n_parents[L];
-        bool ok = lc->sp.ensure(100 * S1 * 4) && lc->rootsum.ensure(wlw * S1 * 4);
+        // an allocation that fails first reclaims what idle streams free: the
+        // retired slots and the work buffer (re-allocated below, to the budget)
+        auto alloc = [&](DevBuf& b, size_t bytes) -> bool {
+            if (b.ensure(bytes)) return true;
+            if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+            c->bury();
+            c->work.release();
+            return b.ensure(bytes);
+        };
+        bool ok = alloc(lc->sp, 100 * S1 * 4) && alloc(lc->rootsum, wlw * S1 * 4);
         if (ok && nl > lc->nodes_cap) {
             // grow geometrically (a sweep's frontier widens over several levels)
             const size_t cap = std::max(nl, lc->nodes_cap + lc->nodes_cap / 4);
             DevBuf ncs, nw;
-            ok = ncs.ensure(cap * 5 * S1 * 4) && nw.ensure(cap * wlw * S1 * 4);
+            if (!c->graveyard.empty()) {  // the other aggregator's retired slot: free it first
+                if (hipStreamSynchronize(c->stream) == hipSuccess) c->bury();
+            }
+            ok = alloc(ncs, cap * 5 * S1 * 4) && alloc(nw, cap * wlw * S1 * 4);
             if (ok) {
                 if (hit) {
                     cin_cs = lc->cs.as<uint32_t>();
@@ -1000,7 +1018,9 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         c->lc[agg_id].drop();
     }
     if (lc) wl = work_layout(p, t, true);
-    const uint64_t budget = default_budget(c);
+    // with the cache on, half of the free HBM: the other aggregator's slot may
+    // still grow at this level
+    const uint64_t budget = (lc && !c->budget) ? default_budget(c) * 2 / 3 : default_budget(c);
     const size_t per_report = wl.words * 4;
     // Plane rows are padded by stride_pad words: with a power-of-two row
     // length every word of a report sits at the same address bits modulo a
