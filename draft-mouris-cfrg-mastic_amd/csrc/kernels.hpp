@@ -1295,3 +1295,47 @@ __global__ __launch_bounds__(256) void k_decide(McParams p, int n, int stride, i
     }
     status_out[r] = st;
 }
+
+// ------------------------------------------------------------- wire encoding
+// Planes -> report-major wire bytes on the device (mastic.py:537-552): row r
+// of the output is the concatenation of up to 3 plane segments (seg[k]:
+// words[k] planes of stride S), i.e. the prep share eval_proof || [jr_part]
+// || [verifier] (encode_vec is little-endian words, the planes' byte order),
+// or an out share (encode_vec of the truncated vector).  One thread per
+// output word, consecutive threads on consecutive words of a row.
+struct RowSegs {
+    const uint32_t* seg[3];
+    int words[3];
+};
+__global__ __launch_bounds__(256) void k_gather_rows(RowSegs sg, int n, int stride, uint32_t* out) {
+    const int row_words = sg.words[0] + sg.words[1] + sg.words[2];
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)n * row_words) return;
+    const int r = (int)(i / row_words);
+    int k = (int)(i - (size_t)r * row_words);
+    int s = 0;
+    while (k >= sg.words[s]) {
+        k -= sg.words[s];
+        s++;
+    }
+    out[i] = sg.seg[s][(size_t)k * stride + r];
+}
+
+// Both aggregators' prep_shares_to_prep + prep_next outcome per report, from
+// k_decide's code, the two query statuses and (weight check with joint
+// randomness) the joint-rand confirmation of each aggregator
+// (mastic.py:364-377): accept = 1 iff all pass.
+__global__ __launch_bounds__(256) void k_accept(int n, int stride, int check_jr, const uint8_t* code,
+                                                const int32_t* st0, const int32_t* st1, const uint8_t* msg,
+                                                const uint32_t* jrs0, const uint32_t* jrs1, uint8_t* accept) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    bool ok = code[r] == 1 && st0[r] == 0 && st1[r] == 0;
+    if (check_jr) {
+        for (int j = 0; j < 8; j++) {
+            const uint32_t m = ld_u32_bytes(msg + (size_t)32 * r + 4 * j);
+            ok = ok && m == jrs0[(size_t)j * stride + r] && m == jrs1[(size_t)j * stride + r];
+        }
+    }
+    accept[r] = ok ? 1 : 0;
+}

@@ -147,6 +147,7 @@ struct mastic_ctx {
     DevBuf pfx_bytes, pfx_meta;
     DevBuf consts;   // alpha^-i table for prove
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
+    DevBuf stage;               // result encoding / decide staging
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
     int n_cus = 256;                     // compute units of the device
@@ -1064,22 +1065,33 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     return 0;
 }
 
-static void put_words(uint8_t* dst, const std::vector<uint32_t>& planes, size_t stride, size_t r, size_t first,
-                      size_t count) {
-    for (size_t k = 0; k < count; k++) {
-        uint32_t w = planes[(first + k) * stride + r];
-        dst[4 * k] = (uint8_t)w;
-        dst[4 * k + 1] = (uint8_t)(w >> 8);
-        dst[4 * k + 2] = (uint8_t)(w >> 16);
-        dst[4 * k + 3] = (uint8_t)(w >> 24);
-    }
+// Report-major wire rows of plane segments into dst (device), on c->stream.
+static int gather_rows(mastic_ctx* c, const RowSegs& sg, size_t n, size_t stride, void* dst) {
+    const size_t words = (size_t)sg.words[0] + sg.words[1] + sg.words[2];
+    if (n == 0 || words == 0) return 0;
+    const size_t total = n * words;
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream, sg, (int)n,
+                       (int)stride, (uint32_t*)dst);
+    HIPCHK(c, hipGetLastError());
+    return 0;
 }
 
-static int fetch(mastic_ctx* c, const DevBuf& b, size_t planes, size_t stride, std::vector<uint32_t>& out) {
-    out.resize(planes * stride);
-    if (planes == 0) return 0;
-    HIPCHK(c, hipMemcpy(out.data(), b.p, planes * stride * 4, hipMemcpyDeviceToHost));
-    return 0;
+// The prep shares of result slot R as wire rows (mastic.py:543-552):
+// eval_proof || [jr_part] || [verifier].
+static RowSegs prep_share_segs(const McParams& p, const Result& R) {
+    RowSegs sg{};
+    sg.seg[0] = R.eval_proof.as<uint32_t>();
+    sg.words[0] = 8;
+    if (R.weight_check) {
+        int k = 1;
+        if (p.joint_rand_len > 0) {
+            sg.seg[k] = R.jr_part.as<uint32_t>();
+            sg.words[k++] = 8;
+        }
+        sg.seg[k] = R.verifier.as<uint32_t>();
+        sg.words[k] = p.verifier_len * p.w32;
+    }
+    return sg;
 }
 
 extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_shares, uint8_t* jr_seeds,
@@ -1089,49 +1101,76 @@ extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_share
     Result& R = c->res[agg_id];
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
     c->tcur = agg_id;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->bury();  // the stream is idle (it joined the sponge stream before k_finalize)
     const McParams& p = c->p;
     const size_t n = R.n, S = R.stride;
+    // Every output is encoded on the GPU into a staging buffer (planes ->
+    // report-major wire bytes) and copied out once: no per-report host loop.
+    auto emit = [&](const RowSegs& sg, void* host) -> int {
+        const size_t bytes = n * 4 * ((size_t)sg.words[0] + sg.words[1] + sg.words[2]);
+        if (!host || bytes == 0) return 0;
+        if (!c->stage.ensure(bytes)) return fail(c, MASTIC_ENOMEM, "out of device memory (result staging)");
+        if (gather_rows(c, sg, n, S, c->stage.p)) return -1;
+        HIPCHK(c, hipMemcpyAsync(host, c->stage.p, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return 0;
+    };
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bury();  // the stream is idle (it joined the sponge stream before k_finalize)
     if (n == 0) return 0;
-    std::vector<uint32_t> ep, ver, jp, js, st, out;
-    int rc = 0;
-    if (prep_shares) {
-        rc |= fetch(c, R.eval_proof, 8, S, ep);
-        if (R.weight_check) {
-            rc |= fetch(c, R.verifier, (size_t)p.verifier_len * p.w32, S, ver);
-            if (p.joint_rand_len > 0) rc |= fetch(c, R.jr_part, 8, S, jp);
-        }
-        if (rc) return rc;
-        const size_t psz = mc_prep_share_size(p, R.weight_check);
-        for (size_t r = 0; r < n; r++) {
-            uint8_t* d = prep_shares + psz * r;
-            put_words(d, ep, S, r, 0, 8);
-            d += 32;
-            if (R.weight_check) {
-                if (p.joint_rand_len > 0) {
-                    put_words(d, jp, S, r, 0, 8);
-                    d += 32;
-                }
-                put_words(d, ver, S, r, 0, (size_t)p.verifier_len * p.w32);
-            }
-        }
-    }
+    if (emit(prep_share_segs(p, R), prep_shares)) return -1;
     if (jr_seeds && !(R.weight_check && p.joint_rand_len > 0)) {
-        memset(jr_seeds, 0, 32 * n);  // no joint rand in this call: the device buffer is all zero
-    } else if (jr_seeds) {
-        if ((rc = fetch(c, R.jr_seed, 8, S, js))) return rc;
-        for (size_t r = 0; r < n; r++) put_words(jr_seeds + 32 * r, js, S, r, 0, 8);
+        memset(jr_seeds, 0, 32 * n);  // no joint rand in this call
+    } else if (emit(RowSegs{{R.jr_seed.as<uint32_t>(), nullptr, nullptr}, {8, 0, 0}}, jr_seeds)) {
+        return -1;
     }
-    if (out_shares) {
-        const size_t ow = (size_t)R.n_prefixes * (1 + p.output_len) * p.w32;
-        if ((rc = fetch(c, R.out, ow, S, out))) return rc;
-        for (size_t r = 0; r < n; r++) put_words(out_shares + 4 * ow * r, out, S, r, 0, ow);
-    }
-    if (status) {
-        if ((rc = fetch(c, R.status, 1, S, st))) return rc;
-        for (size_t r = 0; r < n; r++) status[r] = (int32_t)st[r];
-    }
+    const int ow = R.n_prefixes * (1 + p.output_len) * p.w32;
+    if (emit(RowSegs{{R.out.as<uint32_t>(), nullptr, nullptr}, {ow, 0, 0}}, out_shares)) return -1;
+    if (emit(RowSegs{{(const uint32_t*)R.status.p, nullptr, nullptr}, {1, 0, 0}}, status)) return -1;
+    return 0;
+}
+
+extern "C" int mastic_decide_results(mastic_ctx* c, const uint8_t* app_ctx, size_t ctx_len, uint8_t* accept_out,
+                                     uint8_t* decide_out) {
+    DeviceScope ds_(c);
+    if (!c) return MASTIC_EINVAL;
+    Result &R0 = c->res[0], &R1 = c->res[1];
+    if (!R0.ready || !R1.ready) return fail(c, MASTIC_EINVAL, "decide needs both aggregators' prep_init results");
+    if (R0.n != R1.n || R0.weight_check != R1.weight_check || R0.n_prefixes != R1.n_prefixes)
+        return fail(c, MASTIC_EINVAL, "the two prep_init results are for different batches / agg params");
+    const size_t n = R0.n, S = R0.stride;
+    if (n == 0) return 0;
+    int rc = build_prefixes(c, app_ctx, ctx_len, nullptr, 0);
+    if (rc) return rc;
+    const McParams& p = c->p;
+    const size_t psz = mc_prep_share_size(p, R0.weight_check);
+    // both prep shares as wire rows (k_decide's input), decide, accept
+    const size_t need = 2 * n * psz + 32 * n + 2 * n + 256 + S * 4 * (size_t)std::max(1, p.verifier_len * p.w32);
+    if (!c->stage.ensure(need)) return fail(c, MASTIC_ENOMEM, "out of device memory (decide staging)");
+    uint8_t* ps0 = c->stage.as<uint8_t>();
+    uint8_t* ps1 = ps0 + n * psz;
+    uint8_t* msg = ps1 + n * psz;
+    uint8_t* code = msg + 32 * n;
+    uint8_t* acc = code + n;
+    uint32_t* ver = (uint32_t*)(((uintptr_t)(acc + n) + 255) & ~(uintptr_t)255);  // FLP scratch planes
+    if (gather_rows(c, prep_share_segs(p, R0), n, S, ps0)) return -1;
+    if (gather_rows(c, prep_share_segs(p, R1), n, S, ps1)) return -1;
+    HIPCHK(c, hipMemsetAsync(msg, 0, 32 * n, c->stream));
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (p.field == 64)
+        hipLaunchKernelGGL(k_decide<F64>, grid, dim3(256), 0, c->stream, p, (int)n, (int)S, R0.weight_check, ps0, ps1,
+                           (int)psz, ver, (const PrefixState*)c->pfx.p, msg, code);
+    else
+        hipLaunchKernelGGL(k_decide<F128>, grid, dim3(256), 0, c->stream, p, (int)n, (int)S, R0.weight_check, ps0,
+                           ps1, (int)psz, ver, (const PrefixState*)c->pfx.p, msg, code);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_accept, grid, dim3(256), 0, c->stream, (int)n, (int)S,
+                       (int)(R0.weight_check && p.joint_rand_len > 0), code, (const int32_t*)R0.status.p,
+                       (const int32_t*)R1.status.p, msg, R0.jr_seed.as<uint32_t>(), R1.jr_seed.as<uint32_t>(), acc);
+    HIPCHK(c, hipGetLastError());
+    if (accept_out) HIPCHK(c, hipMemcpyAsync(accept_out, acc, n, hipMemcpyDeviceToHost, c->stream));
+    if (decide_out) HIPCHK(c, hipMemcpyAsync(decide_out, code, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bury();
     return 0;
 }
 

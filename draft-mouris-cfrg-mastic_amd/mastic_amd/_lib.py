@@ -30,7 +30,7 @@ EXPORTS = [
     "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
     "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
     "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
-    "mastic_aggregate_device", "mastic_reports_view",
+    "mastic_aggregate_device", "mastic_reports_view", "mastic_decide_results",
 ]
 
 
@@ -121,6 +121,7 @@ def lib():
                     "mastic_fold_shares": (i32, [P, P, sz, sz, P, P]),
                     "mastic_aggregate_device": (i32, [P, i32, P, P]),
                     "mastic_reports_view": (i32, [P, sz, sz, ctypes.POINTER(P)]),
+                    "mastic_decide_results": (i32, [P, u8p, sz, P, P]),
                     "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3
                                             + [ctypes.POINTER(ctypes.c_double)]),
                     "mastic_work_bytes": (i32, [P, u8p, sz, ctypes.POINTER(ctypes.c_uint64)]),

@@ -156,17 +156,27 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                 mastic.prep_init_device(dev, verify_key, ctx, agg_id, enc)
                 if cached_levels is not None and agg_id == 0 and frontier_cache and mastic.last_prep_was_cached():
                     cached_levels.append(level)
-            shares = []
-            for agg_id in range(2):
-                shares.append(mastic.prep_result(dev, agg_id, enc))
+            if fast:
+                # both aggregators' prep_shares_to_prep + prep_next on the GPU:
+                # the prep shares stay in HBM, only the accept mask comes back
+                (accept, _codes) = mastic.decide_results(ctx, n)
+                alive &= accept == 1
                 if timing is not None:
-                    timing.append(mastic.last_timing3())
-            (msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
-            alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
-            if level == 0 and mastic.JOINT_RAND_LEN > 0:
-                # prep_next (mastic.py:364-377, called at examples.py:67): each
-                # aggregator's joint-rand seed must equal the prep message
-                alive &= joint_rand_confirmed(msgs, shares[0][1], shares[1][1], n)
+                    for agg_id in range(2):
+                        mastic.select_timing(agg_id)
+                        timing.append(mastic.last_timing3())
+            else:
+                shares = []
+                for agg_id in range(2):
+                    shares.append(mastic.prep_result(dev, agg_id, enc))
+                    if timing is not None:
+                        timing.append(mastic.last_timing3())
+                (msgs, valid) = mastic.decide_batch(ctx, enc, shares[0][0], shares[1][0])
+                alive &= (valid == 1) & (shares[0][3] == 0) & (shares[1][3] == 0)
+                if level == 0 and mastic.JOINT_RAND_LEN > 0:
+                    # prep_next (mastic.py:364-377, called at examples.py:67): each
+                    # aggregator's joint-rand seed must equal the prep message
+                    alive &= joint_rand_confirmed(msgs, shares[0][1], shares[1][1], n)
             mask = alive.astype(np.uint8)
             if device_merge:
                 # both shares folded, gathered and merged in HBM (one RCCL call)

@@ -222,6 +222,19 @@ class Mastic:
             _lib.buf(msgs), _lib.buf(valid)))
         return (msgs.tobytes(), valid)
 
+    def decide_results(self, ctx: bytes, n: int):
+        """prep_shares_to_prep + prep_next of both aggregators' last
+        prep_init_device (same reports and agg param) on the GPU
+        (``mastic_decide_results``) -> (accept uint8 array, decide codes)."""
+        acc = np.empty(n, np.uint8)
+        code = np.empty(n, np.uint8)
+        _check(self._ctx, _lib.lib().mastic_decide_results(self._ctx, ctx, len(ctx), _lib.buf(acc), _lib.buf(code)))
+        return (acc, code)
+
+    def select_timing(self, agg_id: int):
+        """Make last_timing* report agg_id's last prep_init (waits for it)."""
+        _check(self._ctx, _lib.lib().mastic_prep_result(self._ctx, agg_id, None, None, None, None))
+
     def aggregate_to(self, agg_id: int, valid, dev_ptr: int):
         """``mastic_aggregate_device``: fold into caller-owned device memory
         (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM."""

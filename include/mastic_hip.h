@@ -129,6 +129,15 @@ int mastic_prep_init(mastic_ctx* ctx, mastic_reports* rep, const uint8_t* verify
  * shares = prep_state[0], encode_vec); status n (0 = ok, <0 = query abort). */
 int mastic_prep_result(mastic_ctx* ctx, int agg_id, uint8_t* prep_shares, uint8_t* jr_seeds, uint8_t* out_shares,
                        int32_t* status);
+/* Both aggregators' prep_shares_to_prep + prep_next (mastic.py:320-377) for
+ * the last mastic_prep_init of agg_id 0 and of agg_id 1 on this ctx (same
+ * reports and agg param, e.g. a heavy-hitters sweep driving both aggregators
+ * on one GPU): the prep shares never leave HBM.  accept_out[i] (n, may be
+ * NULL) = 1 iff the eval proofs agree, the FLP decides true (weight check),
+ * neither query aborted and both joint-rand seeds equal the prep message;
+ * decide_out[i] (n, may be NULL) = the MASTIC_DECIDE_* code. */
+int mastic_decide_results(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_len, uint8_t* accept_out,
+                          uint8_t* decide_out);
 /* Fold the out shares of the last prep_init for agg_id over the reports whose
  * valid[i] != 0 (valid == NULL: all) into agg_share
  * (len(prefixes)*(1+output_len)*field_bytes, encode_vec). */

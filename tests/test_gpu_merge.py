@@ -152,3 +152,39 @@ def test_sweep_device_merge_one_rank_rccl(torch_cuda):
     assert hh_dev == hh_host and hh_host
     assert [(t.level, t.prefixes, t.agg_result) for t in t_dev] == [(t.level, t.prefixes, t.agg_result)
                                                                      for t in t_host]
+
+
+def test_decide_results_on_device_matches_host_decide(torch_cuda):
+    """mastic_decide_results (both aggregators' results decided in HBM) gives
+    the same codes as decide_batch on the downloaded prep shares, and its
+    accept mask folds in the query status and the joint-rand confirmation
+    (a corrupted peer joint-rand part is rejected)."""
+    import mastic_amd
+    from mastic_amd.heavy_hitters import joint_rand_confirmed
+    rng = random.Random(6)
+    m = mastic_amd.MasticHistogram(5, 6, 2)
+    ctx = b"decide"
+    n = 70
+    alphas = [tuple(bool(rng.getrandbits(1)) for _ in range(5)) for _ in range(n)]
+    weights = [rng.randrange(6) for _ in range(n)]
+    nonces = rng.randbytes(16 * n)
+    rands = rng.randbytes(m.RAND_SIZE * n)
+    (pub, in0, in1) = m.shard_batch(ctx, alphas, weights, nonces, rands)
+    isz = m.input_share_size(0)
+    in0 = bytearray(in0)
+    in0[isz * 3 + isz - 1] ^= 0x01  # report 3: leader's peer joint-rand part
+    dev = m.reports_upload(nonces, pub, bytes(in0), in1)
+    vk = rng.randbytes(16)
+    for ap in [(0, ((False,), (True,)), True), (4, tuple(sorted(set(alphas)))[:9], False)]:
+        enc = m.encode_agg_param(ap)
+        for a in range(2):
+            m.prep_init_device(dev, vk, ctx, a, enc)
+        (acc, codes) = m.decide_results(ctx, n)
+        sh = [m.prep_result(dev, a, enc) for a in range(2)]
+        (msgs, valid) = m.decide_batch(ctx, enc, sh[0][0], sh[1][0])
+        assert list(codes) == list(valid)
+        want = (valid == 1) & (sh[0][3] == 0) & (sh[1][3] == 0)
+        if ap[2]:
+            want &= joint_rand_confirmed(msgs, sh[0][1], sh[1][1], n)
+            assert not want[3]
+        assert list(acc == 1) == list(want)
