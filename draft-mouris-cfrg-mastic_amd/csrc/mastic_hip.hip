@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -20,13 +21,29 @@
 
 namespace {
 
+// MASTIC_TRACE_ALLOC=1: log every device allocation / free with its duration (stderr)
+static bool trace_alloc() {
+    static const bool on = [] {
+        const char* e = getenv("MASTIC_TRACE_ALLOC");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
     bool own = true;  // false: a view into another buffer (mastic_reports_view)
     ~DevBuf() { release(); }
     void release() {
-        if (p && own) (void)hipFree(p);
+        if (p && own) {
+            const double t0 = trace_alloc() ? now_ms() : 0;
+            (void)hipFree(p);
+            if (trace_alloc()) fprintf(stderr, "[mastic] free %.3f GB %.1f ms\n", bytes / 1e9, now_ms() - t0);
+        }
         p = nullptr;
         bytes = 0;
         own = true;
@@ -42,13 +59,24 @@ struct DevBuf {
         if (want <= bytes && p) return true;
         release();
         if (want == 0) want = 16;
-        if (hipMalloc(&p, want) != hipSuccess) {
+        const double t0 = trace_alloc() ? now_ms() : 0;
+        const hipError_t e = hipMalloc(&p, want);
+        if (trace_alloc()) fprintf(stderr, "[mastic] malloc %.3f GB %.1f ms%s\n", want / 1e9, now_ms() - t0,
+                                   e == hipSuccess ? "" : " FAILED");
+        if (e != hipSuccess) {
             p = nullptr;
             (void)hipGetLastError();  // callers handle it; keep it out of later launch checks
             return false;
         }
         bytes = want;
         return true;
+    }
+    // ensure() with headroom: buffers that follow a growing size (results,
+    // staging) are re-allocated rarely (a large hipMalloc costs ~1 s per
+    // 50 GB on MI355X)
+    bool grow(size_t want) {
+        if (want <= bytes && p) return true;
+        return ensure(std::max(want, bytes + bytes / 2)) || ensure(want);
     }
     template <class T> T* as() const { return (T*)p; }
 };
@@ -156,6 +184,7 @@ struct mastic_ctx {
     int aes_prio = 0;                    // s_setprio of the AES waves (MASTIC_AES_PRIO)
     int dbg_skip = 0;                    // timing experiments only (MASTIC_DBG_SKIP; results wrong)
     int stride_pad = 64;                 // words of padding per plane row (MASTIC_STRIDE_PAD)
+    size_t work_arena = (size_t)48 << 30;  // minimum size of a new work buffer (MASTIC_WORK_ARENA_GB)
     bool binder_tiled = true;            // tiled level binder buffers (MASTIC_BINDER_TILED=0: planes)
     int absorb_threads = 256;            // threads per binder-sponge workgroup (MASTIC_ABSORB_THREADS)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
@@ -920,10 +949,10 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     R.weight_check = t->weight_check;
     R.n_prefixes = t->n_prefixes;
     const size_t S = R.stride;
-    if (!R.eval_proof.ensure(S * 8 * 4) || !R.status.ensure(S * 4) ||
-        !R.out.ensure(S * 4 * std::max<size_t>(1, (size_t)t->n_prefixes * (1 + p.output_len) * p.w32)) ||
-        !R.verifier.ensure(S * 4 * (size_t)p.verifier_len * p.w32) || !R.jr_part.ensure(S * 32) ||
-        !R.jr_seed.ensure(S * 32))
+    if (!R.eval_proof.grow(S * 8 * 4) || !R.status.grow(S * 4) ||
+        !R.out.grow(S * 4 * std::max<size_t>(1, (size_t)t->n_prefixes * (1 + p.output_len) * p.w32)) ||
+        !R.verifier.grow(S * 4 * (size_t)p.verifier_len * p.w32) || !R.jr_part.grow(S * 32) ||
+        !R.jr_seed.grow(S * 32))
         return fail(c, MASTIC_ENOMEM, "out of device memory (results for %zu reports)", n);
     HIPCHK(c, hipMemsetAsync(R.jr_part.p, 0, S * 32, c->stream));
     HIPCHK(c, hipMemsetAsync(R.jr_seed.p, 0, S * 32, c->stream));
@@ -1030,9 +1059,23 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     size_t by_budget = (budget / per_report) / 64 * 64;
     if (by_budget > pad + 64) by_budget -= pad;  // the padded rows count against the budget too
     size_t chunk = std::min<size_t>(round_up(n, 64), by_budget);
-    if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
-    if (!c->work.ensure(per_report * (chunk + pad)))
-        return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", per_report * (chunk + pad));
+    // The work buffer is an arena kept across calls: a call uses all of its
+    // capacity (even past the budget: it is allocated already), and a new
+    // one is at least c->work_arena bytes (within the budget), so a level
+    // sweep whose trees grow from level to level does not re-allocate it at
+    // every level.
+    const size_t have = c->work.bytes / per_report;
+    if (have >= std::min(chunk, round_up(n, 64)) + pad) {
+        chunk = std::min<size_t>(round_up(n, 64), (have - pad) / 64 * 64);
+    } else {
+        if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
+        const size_t want = per_report * (chunk + pad);
+        const size_t arena = std::max(want, std::min<size_t>(c->work_arena, budget));
+        if (!c->work.ensure(arena) && !c->work.ensure(want))
+            return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", want);
+        chunk = std::min<size_t>(round_up(n, 64), (c->work.bytes / per_report - pad) / 64 * 64);
+    }
+    if (c->budget) chunk = std::min(chunk, std::max<size_t>(by_budget, 64));  // an explicit budget caps chunks
     size_t evi = 0;
     hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
     HIPCHK(c, hipEventRecord(t0, c->stream));
@@ -1108,7 +1151,7 @@ extern "C" int mastic_prep_result(mastic_ctx* c, int agg_id, uint8_t* prep_share
     auto emit = [&](const RowSegs& sg, void* host) -> int {
         const size_t bytes = n * 4 * ((size_t)sg.words[0] + sg.words[1] + sg.words[2]);
         if (!host || bytes == 0) return 0;
-        if (!c->stage.ensure(bytes)) return fail(c, MASTIC_ENOMEM, "out of device memory (result staging)");
+        if (!c->stage.grow(bytes)) return fail(c, MASTIC_ENOMEM, "out of device memory (result staging)");
         if (gather_rows(c, sg, n, S, c->stage.p)) return -1;
         HIPCHK(c, hipMemcpyAsync(host, c->stage.p, bytes, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1145,7 +1188,7 @@ extern "C" int mastic_decide_results(mastic_ctx* c, const uint8_t* app_ctx, size
     const size_t psz = mc_prep_share_size(p, R0.weight_check);
     // both prep shares as wire rows (k_decide's input), decide, accept
     const size_t need = 2 * n * psz + 32 * n + 2 * n + 256 + S * 4 * (size_t)std::max(1, p.verifier_len * p.w32);
-    if (!c->stage.ensure(need)) return fail(c, MASTIC_ENOMEM, "out of device memory (decide staging)");
+    if (!c->stage.grow(need)) return fail(c, MASTIC_ENOMEM, "out of device memory (decide staging)");
     uint8_t* ps0 = c->stage.as<uint8_t>();
     uint8_t* ps1 = ps0 + n * psz;
     uint8_t* msg = ps1 + n * psz;
@@ -1181,7 +1224,7 @@ static int aggregate_impl(mastic_ctx* c, int agg_id, const uint8_t* valid, uint3
     const size_t rows = (size_t)R.n_prefixes * (1 + p.output_len);
     const uint8_t* dv = nullptr;
     if (valid && R.n) {
-        if (!c->agg_valid.ensure(R.n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        if (!c->agg_valid.grow(R.n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
         HIPCHK(c, hipMemcpyAsync(c->agg_valid.p, valid, R.n, hipMemcpyHostToDevice, c->stream));
         dv = c->agg_valid.as<uint8_t>();
     }
@@ -1204,7 +1247,7 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
     const McParams& p = c->p;
     const size_t rows = (size_t)R.n_prefixes * (1 + p.output_len);
-    if (!c->agg_out.ensure(std::max<size_t>(rows, 1) * p.w32 * 4)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+    if (!c->agg_out.grow(std::max<size_t>(rows, 1) * p.w32 * 4)) return fail(c, MASTIC_ENOMEM, "out of device memory");
     int rc = aggregate_impl(c, agg_id, valid, c->agg_out.as<uint32_t>());
     if (rc) return rc;
     if (agg_share && rows)
@@ -1620,6 +1663,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (pw) c->proof_waves = std::max(1, std::min(15, atoi(pw)));
         const char* spd = getenv("MASTIC_STRIDE_PAD");
         if (spd) c->stride_pad = std::max(0, std::min(1 << 20, atoi(spd))) / 64 * 64;
+        const char* wa = getenv("MASTIC_WORK_ARENA_GB");
+        if (wa) c->work_arena = (size_t)std::max(0, atoi(wa)) << 30;
         const char* bt = getenv("MASTIC_BINDER_TILED");
         if (bt) c->binder_tiled = bt[0] != '0';
         const char* at = getenv("MASTIC_ABSORB_THREADS");
