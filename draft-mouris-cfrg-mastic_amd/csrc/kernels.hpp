@@ -496,6 +496,12 @@ struct AesArgs {
     uint32_t* last_w;
     int wp_by_node;
     int in_stride;  // plane stride of cs_in / fr_w_in (the cache's, on a hit; else the work buffer's)
+    // frontier-cache hit (FC only): the AES waves also compute THIS level's
+    // node proofs right after each parent's payloads (no k_node_proof launch)
+    int fuse_proofs;
+    int cur_path_bytes;              // ceil((level + 1) / 8)
+    const uint32_t* cur_child_path;  // [2 * n_parents][8]
+    uint32_t* cur_onehot;            // this level's proof tiles
     // node proofs of the PREVIOUS level (vidpf.py:366-380, :321-323), computed
     // by the workgroup's EVAL_PROOF_WAVES proof waves beside the AES waves
     int pv_level;                   // level - 1
@@ -573,13 +579,14 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     if (threadIdx.x == 0) *next_parent = 0u;
     __syncthreads();
     const int aes_waves = a.aes_waves;
-    if (wave >= aes_waves) {
-        // proof wave: node proofs of level - 1 (children seeds from cs_in)
-        if (a.pv_nodes == 0 || (a.dbg_skip & 1)) return;
+    // Proof waves: node proofs of level - 1 (children seeds from cs_in), then
+    // they help with the parents; with no proofs to do (level 0, a frontier-
+    // cache hit) they walk parents from the start.  No wave returns early: a
+    // cache hit's fused proofs below end with a workgroup barrier.
+    if (wave >= aes_waves && a.pv_nodes > 0 && !(a.dbg_skip & 1)) {
         if (a.proof_prio == 1) __builtin_amdgcn_s_setprio(1);
         if (a.proof_prio == 2) __builtin_amdgcn_s_setprio(2);
         const int nbeg = (blockIdx.y * (EVAL_WAVES - aes_waves) + (wave - aes_waves)) * a.pv_npw;
-        if (nbeg >= a.pv_nodes) return;
         const int nend = min(nbeg + a.pv_npw, a.pv_nodes);
         const int pl_ = a.pv_level;
         uint32_t* ohg = a.pv_onehot + (size_t)blockIdx.x * a.oh_gstride;  // tile group of these 64 reports
@@ -598,14 +605,15 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         if (a.proof_prio) __builtin_amdgcn_s_setprio(0);
         // then help with this workgroup's parents (below)
     }
-    if (a.dbg_skip & 2) return;
-    if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
-    if (a.aes_prio == 2) __builtin_amdgcn_s_setprio(2);
     // Parents of this workgroup: [wp0, wp1), claimed in runs of `run` by
     // every wave through an LDS counter: the proof waves join once their
     // proofs are done, so no wave idles while another still has parents.
     const int wp0 = blockIdx.y * aes_waves * a.ppw;
     const int wp1 = min(wp0 + aes_waves * a.ppw, a.n_parents);
+    if (a.dbg_skip & 2) goto aes_done;
+    {
+    if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (a.aes_prio == 2) __builtin_amdgcn_s_setprio(2);
     const int run = max(1, a.ppw / 8);
     auto claim = [&]() -> int {
         uint32_t o = 0;
@@ -613,7 +621,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         return wp0 + (int)__builtin_amdgcn_readfirstlane(o);
     };
     int rbeg = claim();
-    if (rbeg >= wp1) return;
+    if (rbeg >= wp1) goto aes_done;
     int rend = min(rbeg + run, wp1);
     const int l = a.level;
     const int vl = p.value_len;
@@ -801,6 +809,34 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             }
         }
         pi = nxt;
+    }
+    }
+aes_done:
+    if constexpr (FC) {
+        if (a.fuse_proofs) {
+            // frontier-cache hit: this level's node proofs (vidpf.py:366-380,
+            // :321-323) of the workgroup's children, once all its parents are
+            // done (the child seeds / control bits are in cs_out; the barrier
+            // orders the other waves' stores before these loads).  The VALU-
+            // bound Keccak of one workgroup overlaps the LDS-bound AES of the
+            // others on the CU, and no k_node_proof launch follows.
+            __syncthreads();
+            const int l = a.level;
+            const int nb = 2 * wp0, ne = 2 * wp1;
+            uint32_t* ohg = a.cur_onehot + (size_t)blockIdx.x * a.oh_gstride;
+            const uint32_t lt = (uint32_t)lane * 4u;
+            uint32_t pcw[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)l * 8 + j) * S, lb);
+            for (int node = nb + wave; node < ne; node += EVAL_WAVES) {
+                uint32_t sd[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_out + ((size_t)node * 5 + i) * S, lb);
+                const uint32_t t = pld(a.cs_out + ((size_t)node * 5 + 4) * S, lb);
+                node_proof_one(a.np, a.np_f, p.bits, l, a.cur_path_bytes, sd, a.cur_child_path + node * 8, t, pcw,
+                               [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
+            }
+        }
     }
 }
 

@@ -189,6 +189,7 @@ struct mastic_ctx {
     int absorb_threads = 256;            // threads per binder-sponge workgroup (MASTIC_ABSORB_THREADS)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
+    bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::vector<uint8_t> pfx_key;  // verify key || ctx of the prefix states in pfx (empty: none)
     std::map<std::vector<uint8_t>, Tree*> trees;
@@ -806,6 +807,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.force_slow_blk = c->force_slow_blk;
         a.last_w = (lc && l == t->L) ? plane(wl.lastw) : nullptr;
         a.wp_by_node = hit ? 1 : 0;
+        const bool fuse = hit && c->fuse_proofs && l == t->L;
+        a.fuse_proofs = fuse ? 1 : 0;
+        a.cur_path_bytes = (l + 1 + 7) / 8;
+        a.cur_child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
+        a.cur_onehot = oh_buf(l);
         a.aes_waves = EVAL_WAVES - c->proof_waves;
         a.proof_prio = c->proof_prio;
         a.aes_prio = c->aes_prio;
@@ -846,7 +852,20 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             HIPCHK(c, hipEventRecord(e5, c->stream2));
         }
     }
-    {
+    if (hit && c->fuse_proofs) {
+        // the last level's proofs came from the level kernel's AES waves: its sponges
+        const int l = t->L;
+        hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
+        hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
+        hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
+        HIPCHK(c, hipEventRecord(e0, c->stream));
+        HIPCHK(c, hipEventRecord(e1, c->stream));
+        HIPCHK(c, hipEventRecord(e2, c->stream));
+        HIPCHK(c, hipEventRecord(e3, c->stream));
+        hipEvent_t np_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(np_done, c->stream));
+        if (launch_absorb(l, np_done, e4, e5)) return -1;
+    } else {
         // the last level's node proofs, then its sponges
         const int l = t->L;
         const int nn = 2 * t->n_parents[l];
@@ -1677,6 +1696,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (xp) c->aes_prio = std::max(0, std::min(2, atoi(xp)));
         const char* pp = getenv("MASTIC_PROOF_PRIO");
         if (pp) c->proof_prio = std::max(0, std::min(2, atoi(pp)));
+        const char* fp = getenv("MASTIC_FUSE_PROOFS");
+        if (fp) c->fuse_proofs = fp[0] != '0';
         const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
         c->force_slow_blk = fs ? atoi(fs) : -1;
     }

@@ -173,3 +173,59 @@ def test_cache_across_hbm_chunks(mastic_amd):
         _lib.lib().mastic_set_memory_budget(m_on._ctx, ctypes.c_uint64(0))
         m_on.set_frontier_cache(False)
     assert hits >= 4, hits
+
+
+def test_cache_at_c3_parameters(mastic_amd):
+    """BASELINE config C3's Mastic(256, Count) through a full 256-level
+    threshold sweep with the cache on: every level bit-identical to a cache-off
+    context, sampled reports of deep cached levels against the CPU oracle,
+    and the heavy hitters equal to the plaintext counts."""
+    from mastic_amd.heavy_hitters import compute_heavy_hitters
+    rng = random.Random(81)
+    m_off = mastic_amd.MasticCount(256)
+    m_on = mastic_amd.MasticCount(256)
+    o = _oracle_for(m_off)
+    n = 256
+    (alphas, weights, nonces, rands) = _reports(m_off, rng, n, 6)
+    (pub, in0, in1) = m_off.shard_batch(CTX, alphas, weights, nonces, rands)
+    vk = bytes(rng.getrandbits(8) for _ in range(16))
+    th = {"default": 12}
+    trace = []
+    dev_off = m_off.reports_upload(nonces, pub, in0, in1)
+    hh = compute_heavy_hitters(m_off, CTX, th, dev_off, verify_key=vk, trace=trace)
+    counts = {}
+    for (a, w) in zip(alphas, weights):
+        counts[a] = counts.get(a, 0) + w
+    assert hh == sorted(a for (a, c) in counts.items() if c >= 12) and hh
+    dev_on = m_on.reports_upload(nonces, pub, in0, in1)
+    m_on.set_frontier_cache(True)
+    psz, isz = m_off.public_share_size(), m_off.input_share_size(1)
+    hits = 0
+    targets = [40, 129, 250]  # oracle samples at the first cached level at or past each
+    checked = []
+    try:
+        for lv in trace:
+            if not lv.prefixes:
+                break
+            ap = (lv.level, tuple(lv.prefixes), lv.level == 0)
+            for agg_id in range(2):
+                m_off.prep_init_device(dev_off, vk, CTX, agg_id, ap)
+                m_on.prep_init_device(dev_on, vk, CTX, agg_id, ap)
+                cached = m_on.last_prep_was_cached()
+                hits += cached
+                a = m_off.prep_result(dev_off, agg_id, ap, want_out_shares=True)
+                b = m_on.prep_result(dev_on, agg_id, ap, want_out_shares=True)
+                assert a[0] == b[0] and a[2] == b[2], "level %d agg %d" % (lv.level, agg_id)
+                if agg_id == 1 and cached and targets and lv.level >= targets[0]:
+                    targets.pop(0)
+                    checked.append(lv.level)
+                    for i in (0, n - 1):
+                        cws = o.vidpf.decode_public_share(pub[psz * i:psz * (i + 1)])
+                        isd = o.decode_input_share(1, in1[isz * i:isz * (i + 1)])
+                        (_st, sh) = o.prep_init(vk, CTX, 1, ap, nonces[16 * i:16 * (i + 1)], cws, isd)
+                        enc = o.test_vec_encode_prep_share(sh)
+                        assert b[0][len(enc) * i:len(enc) * (i + 1)] == enc, "level %d report %d" % (lv.level, i)
+    finally:
+        m_on.set_frontier_cache(False)
+    assert hits >= 2 * 200, hits
+    assert len(checked) == 3, checked

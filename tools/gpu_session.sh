@@ -28,7 +28,7 @@ for s in "$@"; do
     cfg=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
     args=${args//+/ }; cfg=${cfg:-c2}
     case $kind in
-        tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=15 ;;
         smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step "bench_${cfg}" 900 python3 -u bench.py --config "$cfg" $args ;;
         stats) step "stats_${cfg}" 900 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args ;;
