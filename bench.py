@@ -639,6 +639,18 @@ def main():
             if tr["config"] == args.config and tr["prefixes"] == len(attrs) and tr["reports"] == n_rep:
                 out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
                 out["roofline"]["traffic_unit"] = "bytes per launch"
+                out["roofline"]["traffic_per_step"] = tr["hbm_read_bytes_per_step"] + tr["hbm_write_bytes_per_step"]
+    # HBM bytes per step, two references (DESIGN.md §4 "HBM traffic"): SURVEY §8d's
+    # algorithmic bytes (inputs and outputs only: correction words, input share,
+    # prep share) and the floor of the level-synchronous schedule, whose level
+    # buffers (child seeds, proofs, frontier payloads, payload differences) must
+    # round-trip HBM because the BFS-ordered binders need a whole level at once
+    wl_b = m.VALUE_LEN * m.field.ENCODED_SIZE
+    alg = (bits * (16 + wl_b + 32) + (2 * bits + 7) // 8 + m.sizes.input_share_size[args.agg_id]
+           + m.prep_share_size(True))
+    floor = nodes * (20 + 10 + 32 + 20) + interior * (3 * wl_b)
+    out["roofline"]["algorithmic_bytes_per_step"] = alg * n_rep
+    out["roofline"]["level_buffer_floor_per_step"] = floor * n_rep
 
     full = cfg.get("full_job", False) if args.full_job < 0 else bool(args.full_job)
     if full and n_total > n_rep:

@@ -1,9 +1,10 @@
+# ad-hoc GPU session (edited per experiment; see tools/gpu_session.sh for the standard steps)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r02_v8; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -2 $O/tests.log
-timeout -k 10 300 python3 bench.py --config c3sweep --steps 1 --warmup 0 --cpu-baseline 0 > $O/c3sweep_fused.log 2>&1 || exit 1
-MASTIC_FUSE_PROOFS=0 timeout -k 10 300 python3 bench.py --config c3sweep --steps 1 --warmup 0 --cpu-baseline 0 > $O/c3sweep_nofuse.log 2>&1 || exit 1
-timeout -k 10 600 python3 bench.py --config c2sweep --steps 1 --warmup 0 --cpu-baseline 0 > $O/c2sweep.log 2>&1 || exit 1
-echo done
+O=gpurun_out/r02_v10; mkdir -p $O
+run() { local n=$1; shift; echo "[$(date +%T)] $n" >> $O/steps.txt; timeout -k 10 600 "$@" > $O/$n.log 2>&1 || { echo "$n failed rc=$?" >> $O/steps.txt; tail -5 $O/$n.log; exit 1; }; }
+run c2sweep_nofuse env MASTIC_FUSE_PROOFS=0 python3 bench.py --config c2sweep --steps 1 --warmup 0 --cpu-baseline 0
+run c3sweep_131072 python3 bench.py --config c3sweep --reports 131072 --steps 1 --warmup 0 --cpu-baseline 0
+run stats_c3sweep_131072 rocprofv3 --kernel-trace --stats -d $O/stats_c3sweep_131072 -o run --output-format csv -- python3 bench.py --config c3sweep --reports 131072 --steps 1 --warmup 0 --cpu-baseline 0
+rm -f $O/stats_c3sweep_131072/run_kernel_trace.csv.gz
+echo done >> $O/steps.txt

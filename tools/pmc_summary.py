@@ -27,12 +27,13 @@ def load(path):
     return dur, n, vals
 
 
-def main(d, kernels=("k_eval_aes<F64>", "k_eval_aes<F128>", "k_node_proof", "k_absorb_pair", "k_absorb")):
+def main(d, suffix="", kernels=("k_eval_aes<F64>", "k_eval_aes<F128>", "k_node_proof", "k_absorb_pair", "k_absorb")):
+    """d: the output directory; suffix: "_<cfg>" for tools/gpu_session.sh pmc:<cfg> passes."""
     out = {}
-    dur, n, sq1 = load(os.path.join(d, "sq1/run_counter_collection.csv"))
-    _, _, sq2 = load(os.path.join(d, "sq2/run_counter_collection.csv"))
-    _, _, fe = load(os.path.join(d, "fetch/run_counter_collection.csv"))
-    _, _, wr = load(os.path.join(d, "write/run_counter_collection.csv"))
+    dur, n, sq1 = load(os.path.join(d, "sq1%s/run_counter_collection.csv" % suffix))
+    _, _, sq2 = load(os.path.join(d, "sq2%s/run_counter_collection.csv" % suffix))
+    _, _, fe = load(os.path.join(d, "fetch%s/run_counter_collection.csv" % suffix))
+    _, _, wr = load(os.path.join(d, "write%s/run_counter_collection.csv" % suffix))
     for k in kernels:
         if k not in dur:
             continue
@@ -61,4 +62,4 @@ def main(d, kernels=("k_eval_aes<F64>", "k_eval_aes<F128>", "k_node_proof", "k_a
 
 
 if __name__ == "__main__":
-    print(json.dumps(main(sys.argv[1]), indent=1))
+    print(json.dumps(main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else ""), indent=1))
