@@ -468,3 +468,43 @@ def test_max_bits_many_prefixes_properties(mastic_amd):
     for (a, w) in zip(alphas, weights):
         want[a] = want.get(a, 0) + w
     assert m.unshard(ap, aggs, n) == [want.get(p, 0) for p in ap[1]]
+
+
+def test_c2_full_prefix_count_oracle_report(mastic_amd):
+    """BASELINE config C2 at its full size: Mastic(32, Sum 255), 10,000 random
+    32-bit candidate prefixes at level 31 (376k tree nodes per report).  64
+    reports through both aggregators: decide valid everywhere, aggregate equal
+    to the plaintext per-attribute sums, and one report's prep share replayed
+    in the CPU oracle at full tree size (about 25 s of CPU)."""
+    rng = random.Random(13)
+    m = mastic_amd.MasticSum(32, 255)
+    attrs = set()
+    while len(attrs) < 10000:
+        attrs.add(tuple(bool(rng.getrandbits(1)) for _ in range(32)))
+    attrs = sorted(attrs)
+    n = 64
+    alphas = [attrs[rng.randrange(len(attrs))] for _ in range(n)]
+    weights = [rng.randrange(256) for _ in range(n)]
+    nonces = bytes(rng.getrandbits(8) for _ in range(16 * n))
+    rands = bytes(rng.getrandbits(8) for _ in range(m.RAND_SIZE * n))
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    ap = (31, tuple(attrs), True)
+    assert m.tree_stats(ap)[0] > 370000
+    vk = bytes(rng.getrandbits(8) for _ in range(16))
+    res = [m.prep_init_batch(vk, CTX, a, ap, nonces, pub, in0 if a == 0 else in1, want_out_shares=False)
+           for a in range(2)]
+    (_msgs, valid) = m.decide_batch(CTX, ap, res[0][0], res[1][0])
+    assert list(valid) == [1] * n
+    aggs = [m.aggregate_device(a, ap) for a in range(2)]
+    want = {}
+    for (a, w) in zip(alphas, weights):
+        want[a] = want.get(a, 0) + w
+    assert m.unshard(ap, aggs, n) == [want.get(p, 0) for p in ap[1]]
+    o = _oracle_for(m)
+    psz, isz = m.public_share_size(), m.input_share_size(0)
+    i = 37
+    cws = o.vidpf.decode_public_share(pub[psz * i:psz * (i + 1)])
+    isd = o.decode_input_share(0, in0[isz * i:isz * (i + 1)])
+    (_st, sh) = o.prep_init(vk, CTX, 0, ap, nonces[16 * i:16 * (i + 1)], cws, isd)
+    enc = o.test_vec_encode_prep_share(sh)
+    assert res[0][0][len(enc) * i:len(enc) * (i + 1)] == enc
