@@ -190,6 +190,7 @@ struct mastic_ctx {
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
+    bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::vector<uint8_t> pfx_key;  // verify key || ctx of the prefix states in pfx (empty: none)
     std::map<std::vector<uint8_t>, Tree*> trees;
@@ -665,22 +666,26 @@ static int choose_eval_ppw(int n_parents, int groups, int aes_waves, int n_cus) 
 }
 
 static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst_off, const uint32_t* src,
-                       size_t src_stride, size_t n, size_t planes) {
+                       size_t src_stride, size_t n, size_t planes, hipStream_t s) {
     if (planes == 0) return 0;
     HIPCHK(c, hipMemcpy2DAsync(dst.as<uint32_t>() + dst_off, dst_stride * 4, src, src_stride * 4, n * 4, planes,
-                               hipMemcpyDeviceToDevice, c->stream));
+                               hipMemcpyDeviceToDevice, s));
     return 0;
 }
 
-// One chunk of reports [base, base + n) of a prep_init.  lc: the frontier
-// cache (or null); on a hit the parents' seeds / payloads are read from
-// cin_cs / cin_w (the cache slot, or its predecessor when the slot grew).
+// One chunk of reports [base, base + n) of a prep_init, in work area W.
+// lc: the frontier cache (or null); on a hit the parents' seeds / payloads
+// are read from cin_cs / cin_w (the cache slot, or its predecessor when the
+// slot grew).  tail: the stream of the chunk's last part (finalize, FLP,
+// result and cache copies): the sponge stream when chunks are pipelined (the
+// next chunk's evaluation, in the other half of the work arena, then
+// overlaps this chunk's last sponges), else the main stream.  sev0: first
+// sync event of this chunk (consecutive pipelined chunks use disjoint ones).
 template <class F>
 static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
                      size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit, const uint32_t* cin_cs,
-                     const uint32_t* cin_w) {
+                     const uint32_t* cin_w, uint32_t* W, hipStream_t tail, size_t sev0) {
     const McParams& p = c->p;
-    uint32_t* W = c->work.as<uint32_t>();
     Planes pl = make_planes(W, wl, n, stride);
     // Every level plane (child seeds, frontier payloads, proof / payload-
     // difference ring, out shares, staged last-level payloads) is written
@@ -718,7 +723,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // seeds 2 slots; proof / payload 3 slots (eval_aes(l) writes payload(l)
     // and proofs(l-1), so it waits absorb(l-3)).  Timing: one (eval, proof,
     // absorb) event triplet per step of the loop below.
-    size_t sev = 0;
+    size_t sev = sev0;
     std::vector<hipEvent_t> abs_done(t->L + 1);
     // tiled level buffers (kernels.hpp AbsorbArgs): words per report group
     // (MASTIC_BINDER_TILED=0: plane layout, i.e. group stride 64, row stride = stride)
@@ -767,7 +772,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     };
     auto to_cache = [&](uint32_t* dst, const uint32_t* src, size_t planes) -> int {
         HIPCHK(c, hipMemcpy2DAsync(dst + base, lc->S * 4, src, (size_t)stride * 4, (size_t)n * 4, planes,
-                                   hipMemcpyDeviceToDevice, c->stream));
+                                   hipMemcpyDeviceToDevice, tail));
         return 0;
     };
     if (hit) {
@@ -895,13 +900,13 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipEventRecord(np_done, c->stream));
         if (launch_absorb(l, np_done, e4, e5)) return -1;
     }
-    HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[t->L], 0));
+    if (tail != c->stream2) HIPCHK(c, hipStreamWaitEvent(tail, abs_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
-    hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl, fa, pfx);
+    hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl, fa, pfx);
     if (t->weight_check) {
         FlpArgs fl{agg_id, t->L};
-        hipLaunchKernelGGL(k_flp_rand<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl, fl, pfx);
-        hipLaunchKernelGGL(k_flp_query<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream, p, pl,
+        hipLaunchKernelGGL(k_flp_rand<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl, fl, pfx);
+        hipLaunchKernelGGL(k_flp_query<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl,
                            flp_consts<F>(p));
     }
     HIPCHK(c, hipGetLastError());
@@ -919,15 +924,16 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // results -> the agg_id slot (plane stride = all reports)
     Result& R = c->res[agg_id];
     int rc = 0;
-    rc |= copy_planes(c, R.eval_proof, R.stride, base, pl.eval_proof, stride, n, 8);
-    rc |= copy_planes(c, R.status, R.stride, base, (const uint32_t*)pl.status, stride, n, 1);
+    rc |= copy_planes(c, R.eval_proof, R.stride, base, pl.eval_proof, stride, n, 8, tail);
+    rc |= copy_planes(c, R.status, R.stride, base, (const uint32_t*)pl.status, stride, n, 1, tail);
     rc |= copy_planes(c, R.out, R.stride, base, plane(wl.out), stride, n,
-                      (size_t)t->n_prefixes * (1 + p.output_len) * p.w32);
+                      (size_t)t->n_prefixes * (1 + p.output_len) * p.w32, tail);
     if (t->weight_check) {
-        rc |= copy_planes(c, R.verifier, R.stride, base, pl.verifier, stride, n, (size_t)p.verifier_len * p.w32);
+        rc |= copy_planes(c, R.verifier, R.stride, base, pl.verifier, stride, n, (size_t)p.verifier_len * p.w32,
+                          tail);
         if (p.joint_rand_len > 0) {
-            rc |= copy_planes(c, R.jr_part, R.stride, base, pl.jr_part, stride, n, 8);
-            rc |= copy_planes(c, R.jr_seed, R.stride, base, pl.jr_seed, stride, n, 8);
+            rc |= copy_planes(c, R.jr_part, R.stride, base, pl.jr_part, stride, n, 8, tail);
+            rc |= copy_planes(c, R.jr_seed, R.stride, base, pl.jr_seed, stride, n, 8, tail);
         }
     }
     return rc;
@@ -1095,19 +1101,42 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         chunk = std::min<size_t>(round_up(n, 64), (c->work.bytes / per_report - pad) / 64 * 64);
     }
     if (c->budget) chunk = std::min(chunk, std::max<size_t>(by_budget, 64));  // an explicit budget caps chunks
+    // Several chunks: pipeline them through the two halves of the work arena
+    // (chunk k+1 evaluates in one half while chunk k's last sponges, finalize
+    // and copies run on the sponge stream over the other).
+    const size_t half_cap = c->work.bytes / 2 / per_report;  // reports (padding rows included) per half
+    const bool pipe = c->chunk_pipeline && n > chunk && chunk >= 128 && half_cap >= pad + 64;
+    if (pipe) chunk = std::min(chunk / 2, half_cap - pad) / 64 * 64;
+    const size_t half = c->work.bytes / 2 / 4 / 64 * 64;  // words: second half's offset
+    const size_t nsev = 2 * (size_t)t->L + 8;           // sync events one chunk uses
     size_t evi = 0;
     hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
     HIPCHK(c, hipEventRecord(t0, c->stream));
-    for (size_t b = 0; b < n; b += chunk) {
+    hipEvent_t half_free[2] = {get_sync_event(c, 2 * nsev), get_sync_event(c, 2 * nsev + 1)};
+    size_t k = 0;
+    for (size_t b = 0; b < n; b += chunk, k++) {
         const int nn = (int)std::min(chunk, n - b);
         const int stride = (int)(round_up(nn, 64) + pad);
-        rc = p.field == 64 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w)
-                           : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w);
+        const int h = pipe ? (int)(k & 1) : 0;
+        if (pipe && k >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, half_free[h], 0));
+        uint32_t* W = c->work.as<uint32_t>() + h * half;
+        hipStream_t tail = pipe ? c->stream2 : c->stream;
+        rc = p.field == 64
+                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, tail, h * nsev)
+                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, tail,
+                                   h * nsev);
         if (rc) {
             for (void* q : retire_after) c->graveyard.push_back(q);
             if (lc) lc->drop();
             return rc;
         }
+        if (pipe) HIPCHK(c, hipEventRecord(half_free[h], c->stream2));
+    }
+    if (pipe) {
+        // later work on the main stream (results, aggregate, the next call) sees every chunk's tail
+        hipEvent_t done = get_sync_event(c, 2 * nsev + 2);
+        HIPCHK(c, hipEventRecord(done, c->stream2));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, done, 0));
     }
     for (void* q : retire_after) c->graveyard.push_back(q);
     if (lc) {
@@ -1696,6 +1725,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (xp) c->aes_prio = std::max(0, std::min(2, atoi(xp)));
         const char* pp = getenv("MASTIC_PROOF_PRIO");
         if (pp) c->proof_prio = std::max(0, std::min(2, atoi(pp)));
+        const char* cp = getenv("MASTIC_CHUNK_PIPELINE");
+        if (cp) c->chunk_pipeline = cp[0] != '0';
         const char* fp = getenv("MASTIC_FUSE_PROOFS");
         if (fp) c->fuse_proofs = fp[0] != '0';
         const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");

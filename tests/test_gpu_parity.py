@@ -260,11 +260,14 @@ def test_empty_ctx_and_single_prefix(mastic_amd):
     _check_against_oracle(m, o, b"", bytes(32), ap, alphas, weights, nonces, rands)
 
 
-def test_chunked_batches_equal_unchunked(mastic_amd):
-    """Reports processed in several HBM-budget chunks give identical results."""
+@pytest.mark.parametrize("chunk_groups,n", [(1, 150), (4, 600)], ids=["64-report chunks", "pipelined halves"])
+def test_chunked_batches_equal_unchunked(mastic_amd, chunk_groups, n):
+    """Reports processed in several HBM-budget chunks give identical results
+    (with >= 128-report chunks the chunks are pipelined through the two halves
+    of the work arena, their tails on the sponge stream)."""
     rng = random.Random(9)
     m = mastic_amd.MasticCount(8)
-    (alphas, weights, nonces, rands) = _random_reports(m, rng, 150)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, n)
     (pub, in0, _in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
     ap = _random_agg_param(m, rng, alphas, 7, 20, True)
     vk = bytes(32)
@@ -276,7 +279,8 @@ def test_chunked_batches_equal_unchunked(mastic_amd):
     per = ctypes.c_uint64()
     assert _lib.lib().mastic_work_bytes(m._ctx, enc, len(enc), ctypes.byref(per)) == 0
     try:
-        _lib.lib().mastic_set_memory_budget(m._ctx, 64 * per.value + 1000)  # -> 64-report chunks
+        # -> 64-report chunks, or 256-report chunks pipelined as 128-report halves
+        _lib.lib().mastic_set_memory_budget(m._ctx, (64 * chunk_groups + 64) * per.value + 1000)
         m2 = m.prep_init_batch(vk, CTX, 0, ap, nonces, pub, in0)
     finally:
         _lib.lib().mastic_set_memory_budget(m._ctx, 0)
