@@ -516,6 +516,13 @@ struct AesArgs {
     const PrefixState* np;          // node-proof prefix state
     int np_f;                       // its fill position
     int aes_waves;                  // waves [0, aes_waves) walk parents, the rest are proof waves
+    int par_waves;                  // items per workgroup = par_waves * ppw (aes_waves, or all 16 waves)
+    // Work items: each parent's payload elements in n_split chunks of
+    // split_len (Field128 circuits with large VALUE_LEN and an identity-like
+    // truncation, tgroup == 1: a C5 parent is 2 x 1,028 AES blocks); an item
+    // recomputes its parent's 4 extend / convert-seed blocks.  1 = whole parents.
+    int n_split;
+    int split_len;
     int proof_prio;                 // s_setprio of the proof waves
     int aes_prio;                   // s_setprio of the AES waves
     int dbg_skip;                   // timing experiments only (results wrong): 1 = no proof work, 2 = no AES work
@@ -608,8 +615,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     // Parents of this workgroup: [wp0, wp1), claimed in runs of `run` by
     // every wave through an LDS counter: the proof waves join once their
     // proofs are done, so no wave idles while another still has parents.
-    const int wp0 = blockIdx.y * aes_waves * a.ppw;
-    const int wp1 = min(wp0 + aes_waves * a.ppw, a.n_parents);
+    const int wp0 = blockIdx.y * a.par_waves * a.ppw;                  // items
+    const int wp1 = min(wp0 + a.par_waves * a.ppw, a.n_parents * a.n_split);
     if (a.dbg_skip & 2) goto aes_done;
     {
     if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -645,7 +652,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             for (int i = 0; i < 4; i++) ps[i] = pld(pl.key + (size_t)i * S, lb);
             pctrl = a.agg_id;
         } else {
-            const int pn = a.parent_node[pi];
+            const int pn = a.parent_node[pi / a.n_split];  // pi: a work item here
 #pragma unroll
             for (int i = 0; i < 4; i++) ps[i] = pld(a.cs_in + ((size_t)pn * 5 + i) * S_in, lb);
             pctrl = pld(a.cs_in + ((size_t)pn * 5 + 4) * S_in, lb);
@@ -653,15 +660,19 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     };
     uint32_t nps[4], npctrl;
     load_parent(rbeg, nps, npctrl);
-    for (int pi = rbeg; pi >= 0;) {
+    for (int item = rbeg; item >= 0;) {
+        const int pi = item / a.n_split;        // parent
+        const int ch = item - pi * a.n_split;  // element chunk of it
+        const int e_lo = ch * a.split_len;
+        const int e_hi = min(p.value_len, e_lo + a.split_len);
         // The key schedules are re-read from LDS (one ds_read_b128 per round):
         // without the barrier the compiler hoists all 22 reads out of the loop
         // and pins 88 VGPRs.
         asm volatile("" ::: "memory");
         uint32_t ps[4] = {nps[0], nps[1], nps[2], nps[3]};
         const uint32_t pctrl = npctrl;
-        // next parent: the rest of this run, else a new run
-        int nxt = pi + 1;
+        // next item: the rest of this run, else a new run
+        int nxt = item + 1;
         if (nxt == rend) {
             rbeg = claim();
             rend = min(rbeg + run, wp1);
@@ -685,14 +696,16 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             tc1 ^= (ccw >> 1) & 1u;
         }
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
-        const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
+        if (ch == 0) {
+            const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            pst(a.cs_out + (n0 + i) * S, lb, ns0[i]);
-            pst(a.cs_out + (n1 + i) * S, lb, ns1[i]);
+            for (int i = 0; i < 4; i++) {
+                pst(a.cs_out + (n0 + i) * S, lb, ns0[i]);
+                pst(a.cs_out + (n1 + i) * S, lb, ns1[i]);
+            }
+            pst(a.cs_out + (n0 + 4) * S, lb, tc0);
+            pst(a.cs_out + (n1 + 4) * S, lb, tc1);
         }
-        pst(a.cs_out + (n0 + 4) * S, lb, tc0);
-        pst(a.cs_out + (n1 + 4) * S, lb, tc1);
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
         const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
         const int row = 1 + p.output_len;
@@ -749,7 +762,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         int wpi = pi;
         if constexpr (FC) wpi = a.wp_by_node ? a.parent_node[pi] : pi;
         auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, wpi * vl + e, S_in, r) : F::zero(); };
-        int e_fast = 0;  // elements completed by the fast path
+        int e_fast = e_lo;  // elements completed by the fast path
         if constexpr (!QUAD) {
             // Fast path: block b (counter b + 1) of each child's convert stream
             // holds Field64 candidates 2b and 2b + 1, or Field128 candidate b
@@ -761,11 +774,11 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             // stream below redoes this parent from that element on (elements
             // before it are unaffected by the rejection).
             constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
-            const int nblk = (vl + EPB - 1) / EPB;
-            for (int b = 0; b < nblk; b++) {
+            const int nblk = (e_hi + EPB - 1) / EPB;  // (e_lo is a multiple of EPB)
+            for (int b = e_lo / EPB; b < nblk; b++) {
                 asm volatile("" ::: "memory");
                 const int e = EPB * b;
-                const bool two = EPB == 2 && e + 1 < vl;
+                const bool two = EPB == 2 && e + 1 < e_hi;
                 const int e1 = two ? e + 1 : e;  // uniform clamp
                 const E cwa = load_cw(e), wpa = load_wp(e);
                 E cwb = cwa, wpb = wpa;
@@ -788,27 +801,29 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 e_fast = e + 1 + (two ? 1 : 0);
             }
         }
-        if (e_fast < vl) {
+        if (e_fast < e_hi) {
             // exact next_vec streams (rejection sampling), element by element
-            // from e_fast on; elements before it were emitted by the fast path
+            // from the stream's start (a rejection shifts every later element)
+            // up to e_hi, emitting from e_fast on; elements before it were
+            // emitted by the fast path
             typename EvalStream<F, QUAD>::type st0, st1;
             st0.init(cs0);
             st1.init(cs1);
             constexpr int G = EvalStream<F, QUAD>::type::GROUP;
-            for (int e0 = 0; e0 < vl; e0 += G) {
+            for (int e0 = 0; e0 < e_hi; e0 += G) {
                 asm volatile("" ::: "memory");
-                st0.refill(st1, vl - e0, TL, rkc);
+                st0.refill(st1, e_hi - e0, TL, rkc);
 #pragma unroll
                 for (int i = 0; i < G; i++) {
                     const int e = e0 + i;
-                    if (e >= vl) break;
+                    if (e >= e_hi) break;
                     const E x0 = st0.next(TL, rkc);
                     const E x1 = st1.next(TL, rkc);
                     if (e >= e_fast) emit(e, x0, x1, load_cw(e), load_wp(e));
                 }
             }
         }
-        pi = nxt;
+        item = nxt;
     }
     }
 aes_done:

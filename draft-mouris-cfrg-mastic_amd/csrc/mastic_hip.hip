@@ -191,6 +191,8 @@ struct mastic_ctx {
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
+    int par_waves = 0;           // waves' worth of parents per level-kernel workgroup (0 = by field; MASTIC_PAR_WAVES)
+    int split_elems = 128;       // Field128 payload elements per level-kernel work item (MASTIC_SPLIT_ELEMS, 0 = off)
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::vector<uint8_t> pfx_key;  // verify key || ctx of the prefix states in pfx (empty: none)
     std::map<std::vector<uint8_t>, Tree*> trees;
@@ -798,7 +800,21 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.level = l;
         a.agg_id = agg_id;
         a.n_parents = np_;
-        a.ppw = choose_eval_ppw(np_, groups, EVAL_WAVES - c->proof_waves, c->n_cus);
+        // parents per workgroup: par_waves x ppw.  With few, large parents
+        // (Field128 circuits: 68-1,028 AES blocks per node) every wave of the
+        // workgroup gets parents; with many small ones the proof waves only
+        // mop up after their proofs (MASTIC_PAR_WAVES overrides)
+        const int par_waves = c->par_waves > 0 ? c->par_waves : (p.field == 128 ? EVAL_WAVES : EVAL_WAVES - c->proof_waves);
+        // large Field128 payloads: work items of up to split_elems elements
+        // (kernels.hpp AesArgs::n_split; needs tgroup == 1)
+        a.n_split = 1;
+        a.split_len = p.value_len;
+        if (p.field == 128 && p.tgroup == 1 && c->split_elems > 0 && p.value_len > c->split_elems) {
+            a.n_split = (p.value_len + c->split_elems - 1) / c->split_elems;
+            a.split_len = (p.value_len + a.n_split - 1) / a.n_split;
+        }
+        const int n_items = np_ * a.n_split;
+        a.ppw = choose_eval_ppw(n_items, groups, par_waves, c->n_cus);
         a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
@@ -812,16 +828,17 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.force_slow_blk = c->force_slow_blk;
         a.last_w = (lc && l == t->L) ? plane(wl.lastw) : nullptr;
         a.wp_by_node = hit ? 1 : 0;
-        const bool fuse = hit && c->fuse_proofs && l == t->L;
+        const bool fuse = hit && c->fuse_proofs && l == t->L && a.n_split == 1;
         a.fuse_proofs = fuse ? 1 : 0;
         a.cur_path_bytes = (l + 1 + 7) / 8;
         a.cur_child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
         a.cur_onehot = oh_buf(l);
         a.aes_waves = EVAL_WAVES - c->proof_waves;
+        a.par_waves = par_waves;
         a.proof_prio = c->proof_prio;
         a.aes_prio = c->aes_prio;
         a.dbg_skip = c->dbg_skip;
-        const int gy = (np_ + a.aes_waves * a.ppw - 1) / (a.aes_waves * a.ppw);
+        const int gy = (n_items + a.par_waves * a.ppw - 1) / (a.par_waves * a.ppw);
         a.pv_level = l - 1;
         a.pv_nodes = (l > 0 && !hit) ? 2 * t->n_parents[l - 1] : 0;  // hit: level L-1's proofs are cached
         a.pv_npw = (a.pv_nodes + gy * c->proof_waves - 1) / (gy * c->proof_waves);
@@ -857,7 +874,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             HIPCHK(c, hipEventRecord(e5, c->stream2));
         }
     }
-    if (hit && c->fuse_proofs) {
+    if (hit && c->fuse_proofs && !(p.field == 128 && p.tgroup == 1 && c->split_elems > 0 &&
+                                  p.value_len > c->split_elems)) {
         // the last level's proofs came from the level kernel's AES waves: its sponges
         const int l = t->L;
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
@@ -1725,6 +1743,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (xp) c->aes_prio = std::max(0, std::min(2, atoi(xp)));
         const char* pp = getenv("MASTIC_PROOF_PRIO");
         if (pp) c->proof_prio = std::max(0, std::min(2, atoi(pp)));
+        const char* se = getenv("MASTIC_SPLIT_ELEMS");
+        if (se) c->split_elems = std::max(0, atoi(se));
+        const char* pw2 = getenv("MASTIC_PAR_WAVES");
+        if (pw2) c->par_waves = std::max(1, std::min(EVAL_WAVES, atoi(pw2)));
         const char* cp = getenv("MASTIC_CHUNK_PIPELINE");
         if (cp) c->chunk_pipeline = cp[0] != '0';
         const char* fp = getenv("MASTIC_FUSE_PROOFS");

@@ -512,3 +512,24 @@ def test_c2_full_prefix_count_oracle_report(mastic_amd):
     (_st, sh) = o.prep_init(vk, CTX, 0, ap, nonces[16 * i:16 * (i + 1)], cws, isd)
     enc = o.test_vec_encode_prep_share(sh)
     assert res[0][0][len(enc) * i:len(enc) * (i + 1)] == enc
+
+
+@pytest.mark.parametrize("blk", [-1, 0, 150, 250])
+def test_field128_element_split_work_items(mastic_amd, blk, monkeypatch):
+    """Large Field128 payloads (VALUE_LEN 301 > 128) are evaluated as work
+    items of ~101 elements each (three per parent, each recomputing its
+    parent's extend / convert-seed blocks).  Every output against the oracle,
+    also with the exact-stream handover forced inside the 1st / 2nd / 3rd
+    chunk (the exact stream restarts from element 0 and emits only its
+    chunk's elements)."""
+    if blk >= 0:
+        monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
+    rng = random.Random(400 + blk)
+    m = mastic_amd.MasticSumVec(4, 300, 1, 10)
+    assert m.VALUE_LEN == 301
+    o = _oracle_for(m)
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, 3)
+    vk = bytes(rng.getrandbits(8) for _ in range(16))
+    for (level, nprefix, wc) in [(0, 2, True), (3, 4, False)]:
+        ap = _random_agg_param(m, rng, alphas, level, nprefix, wc)
+        _check_against_oracle(m, o, CTX, vk, ap, alphas, weights, nonces, rands, check_shard=(level == 0))
