@@ -192,7 +192,10 @@ struct mastic_ctx {
     bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
     int par_waves = 0;           // waves' worth of parents per level-kernel workgroup (0 = by field; MASTIC_PAR_WAVES)
-    int split_elems = 128;       // Field128 payload elements per level-kernel work item (MASTIC_SPLIT_ELEMS, 0 = off)
+    // Field128 payload elements per level-kernel work item (MASTIC_SPLIT_ELEMS;
+    // 0 = whole parents, the default: splitting C5's parents into 9 items
+    // measured 3-6 % slower, its step being bound by the binder sponges)
+    int split_elems = 0;
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::vector<uint8_t> pfx_key;  // verify key || ctx of the prefix states in pfx (empty: none)
     std::map<std::vector<uint8_t>, Tree*> trees;
@@ -800,11 +803,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.level = l;
         a.agg_id = agg_id;
         a.n_parents = np_;
-        // parents per workgroup: par_waves x ppw.  With few, large parents
-        // (Field128 circuits: 68-1,028 AES blocks per node) every wave of the
-        // workgroup gets parents; with many small ones the proof waves only
-        // mop up after their proofs (MASTIC_PAR_WAVES overrides)
-        const int par_waves = c->par_waves > 0 ? c->par_waves : (p.field == 128 ? EVAL_WAVES : EVAL_WAVES - c->proof_waves);
+        // items per workgroup: par_waves x ppw, par_waves = the AES waves (the
+        // proof waves mop up after their proofs).  MASTIC_PAR_WAVES=16 hands
+        // all waves parents from the start: measured neutral on C4 and C2 and
+        // 3 % slower on C5 (profiles/r02_v12_ab_level_kernel.json)
+        const int par_waves = c->par_waves > 0 ? c->par_waves : EVAL_WAVES - c->proof_waves;
         // large Field128 payloads: work items of up to split_elems elements
         // (kernels.hpp AesArgs::n_split; needs tgroup == 1)
         a.n_split = 1;

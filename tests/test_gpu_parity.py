@@ -522,6 +522,7 @@ def test_field128_element_split_work_items(mastic_amd, blk, monkeypatch):
     also with the exact-stream handover forced inside the 1st / 2nd / 3rd
     chunk (the exact stream restarts from element 0 and emits only its
     chunk's elements)."""
+    monkeypatch.setenv("MASTIC_SPLIT_ELEMS", "128")  # (off by default)
     if blk >= 0:
         monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
     rng = random.Random(400 + blk)

@@ -8,8 +8,9 @@ run c2sweep python3 bench.py --config c2sweep --steps 1 --warmup 0 --cpu-baselin
 run c3sweep python3 bench.py --config c3sweep --steps 1 --warmup 0 --cpu-baseline 0
 for c in c5 c4; do
 run ${c}_pw16 python3 bench.py --config $c --steps 3 --warmup 1 --cpu-baseline 0
-run ${c}_pw8 env MASTIC_PAR_WAVES=8 python3 bench.py --config $c --steps 3 --warmup 1 --cpu-baseline 0
+run ${c}_pw8 env MASTIC_PAR_WAVES=8 MASTIC_SPLIT_ELEMS=0 python3 bench.py --config $c --steps 3 --warmup 1 --cpu-baseline 0
 done
+run c5_nosplit env MASTIC_SPLIT_ELEMS=0 python3 bench.py --config c5 --steps 3 --warmup 1 --cpu-baseline 0
 B="python3 bench.py --config c2 --steps 4 --warmup 1 --cpu-baseline 0 --full-job 0 --total-reports 24576"
 run c2_pw8 $B
 run c2_pw16 env MASTIC_PAR_WAVES=16 $B
