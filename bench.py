@@ -63,10 +63,10 @@ CONFIGS = {
                          "32-bit attributes, weights uniform 0..255, threshold 0.05% of the expected total "
                          "weight), both aggregators per level, weight check at level 0; run with --steps 1 "
                          "--warmup 0"),
-    "c4": dict(circuit="Histogram", kw=dict(bits=64, length=64, chunk_length=8), prefixes=1000, reports=12288,
+    "c4": dict(circuit="Histogram", kw=dict(bits=64, length=64, chunk_length=8), prefixes=1000, reports=16384,
                desc="C4: Mastic(BITS=64, Histogram length=64 chunk 8, Field128) prep_init+aggregate, level 63"),
     "c5": dict(circuit="SumVec", kw=dict(bits=32, length=1024, sum_vec_bits=1, chunk_length=32), prefixes=100,
-               reports=8192,
+               reports=16384,
                desc="C5: Mastic(BITS=32, SumVec length=1024 bits=1 chunk 32, Field128) prep_init+aggregate, "
                     "level 31"),
 }

@@ -55,6 +55,11 @@ MH_D void pst(uint32_t* p, uint32_t lane_bytes, uint32_t v) {
 // Word `soff / 4` of a block of planes: one descriptor per block (rs, uniform)
 // and the uniform plane offset in soffset, so a 43-plane block costs 4 SGPRs
 // for the descriptor instead of one descriptor per plane.
+// (the binder sponges' block loads: a stream read once; MASTIC_SPONGE_LOAD_AUX
+// sets their cache policy bits -- gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+#ifndef MASTIC_SPONGE_LOAD_AUX
+#define MASTIC_SPONGE_LOAD_AUX 0
+#endif
 MH_D uint32_t pld_so(__amdgpu_buffer_rsrc_t rs, uint32_t lane_bytes, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b32(rs, lane_bytes, soff, 0);
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, lane_bytes, soff, MASTIC_SPONGE_LOAD_AUX);
 }

@@ -1054,8 +1054,17 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         };
         bool ok = alloc(lc->sp, 100 * S1 * 4) && alloc(lc->rootsum, wlw * S1 * 4);
         if (ok && nl > lc->nodes_cap) {
-            // grow geometrically (a sweep's frontier widens over several levels)
-            const size_t cap = std::max(nl, lc->nodes_cap + lc->nodes_cap / 4);
+            // grow geometrically (a sweep's frontier widens over several
+            // levels), and while HBM is plentiful straight to up to 4x the
+            // need within a fifth of the free memory: each large hipMalloc
+            // costs ~1 s per 50 GB, so a 1M-report sweep should grow its
+            // slots a couple of times, not at every level
+            size_t cap = std::max(nl, lc->nodes_cap + lc->nodes_cap / 4);
+            size_t freeb = 0, totalb = 0;
+            if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+                const size_t per_node = (5 + wlw) * S1 * 4;
+                cap = std::max(cap, std::min(4 * nl, freeb / 5 / per_node));
+            }
             DevBuf ncs, nw;
             if (!c->graveyard.empty()) {  // the other aggregator's retired slot: free it first
                 if (hipStreamSynchronize(c->stream) == hipSuccess) c->bury();
