@@ -390,6 +390,156 @@ MH_D void aes128_encrypt(const AesPerm& T, const RK& rk, uint32_t s[4]) {
     for (int c = 0; c < 4; c++) s[c] = x[0][c];
 }
 
+// ---- counter groups: rounds 1 and 2 shared by the blocks of one seed -----
+// The blocks of one XofFixedKeyAes128 stream differ only in the counter, and
+// the counter enters sigma(seed ^ le128(ctr)) = (s2, s3, s2 ^ s0 ^ ctr, s3 ^ s1)
+// in word 2 alone.  Blocks whose counters agree above bit 7 therefore share 15
+// of the 16 round-1 S-box inputs (all but byte 8), so 3 of the 4 round-1
+// output columns and, in round 2, 3 of the 4 lookups of every column: per
+// block, rounds 1 and 2 need 1 + 4 table lookups instead of 32 (27 of the 160
+// lookups of a block, and their address / XOR work).  The shared part is
+// computed once per (seed, ctr >> 8) by ctr_group_init; ctr_blocks_n finishes
+// N blocks from their groups in lockstep.  (The well-known first-rounds
+// precomputation of AES counter mode, applied per seed.)
+static_assert(AES_T4, "counter groups assume the four-table layout");
+struct AesCtrGroup {
+    uint32_t a;     // LDS address of T0[round-0 byte 8] for counter low byte 0
+    uint32_t p2;    // round-1 column 2 without its T0 lookup
+    uint32_t q[4];  // round-2 columns without their lookup of round-1 column 2
+};
+
+// The shared part of N groups (seeds seed[j], counters ctr_hi[j] & ~0xff) in
+// lockstep: 15 round-1 and 12 round-2 lookups per group.
+template <int N, class RK>
+MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (&seed)[N], const uint32_t (&ctr_hi)[N],
+                         AesCtrGroup* const (&g)[N]) {
+    static_assert(N == 1 || N == 2, "N = 1 or 2");
+    const uint4 k0 = rk(0), k1 = rk(1), k2 = rk(2);
+    uint32_t L[16 * N];  // 15 used per group
+    uint32_t a2v[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t* sd = seed[j];
+        const uint32_t a0 = sd[2] ^ k0.x, a1 = sd[3] ^ k0.y;
+        const uint32_t a2 = sd[2] ^ sd[0] ^ (ctr_hi[j] & ~0xffu) ^ k0.z, a3 = sd[3] ^ sd[1] ^ k0.w;
+        a2v[j] = a2;
+        uint32_t* l = L + 16 * j;
+        // round 1: columns 0, 1, 3 complete, column 2 without T0[a2.b0]
+        l[0] = lds_read_asm(T.a0<0>(a0));
+        l[1] = lds_read_asm(T.a1<1>(a1));
+        l[2] = lds_read_asm(T.a2<2>(a2));
+        l[3] = lds_read_asm(T.a3<3>(a3));
+        l[4] = lds_read_asm(T.a0<0>(a1));
+        l[5] = lds_read_asm(T.a1<1>(a2));
+        l[6] = lds_read_asm(T.a2<2>(a3));
+        l[7] = lds_read_asm(T.a3<3>(a0));
+        l[8] = lds_read_asm(T.a1<1>(a3));
+        l[9] = lds_read_asm(T.a2<2>(a0));
+        l[10] = lds_read_asm(T.a3<3>(a1));
+        l[11] = lds_read_asm(T.a0<0>(a3));
+        l[12] = lds_read_asm(T.a1<1>(a0));
+        l[13] = lds_read_asm(T.a2<2>(a1));
+        l[14] = lds_read_asm(T.a3<3>(a2));
+        l[15] = 0u;
+    }
+    aes_pin<N>(L);
+    uint32_t t[N][4];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t* l = L + 16 * j;
+        t[j][0] = xor3_u32(xor3_u32(l[0], l[1], l[2]), l[3], k1.x);
+        t[j][1] = xor3_u32(xor3_u32(l[4], l[5], l[6]), l[7], k1.y);
+        t[j][3] = xor3_u32(xor3_u32(l[11], l[12], l[13]), l[14], k1.w);
+        g[j]->p2 = xor3_u32(l[8], l[9], l[10]) ^ k1.z;
+        g[j]->a = T.a0<0>(a2v[j]);
+    }
+    // round 2: column c reads one byte of round-1 column 2 (c = 0: byte 2,
+    // 1: byte 1, 2: byte 0, 3: byte 3); the other three lookups are shared
+    uint32_t M[16 * N];  // 12 used per group
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t t0 = t[j][0], t1 = t[j][1], t3 = t[j][3];
+        uint32_t* m = M + 16 * j;
+        m[0] = lds_read_asm(T.a0<0>(t0));
+        m[1] = lds_read_asm(T.a1<1>(t1));
+        m[2] = lds_read_asm(T.a3<3>(t3));
+        m[3] = lds_read_asm(T.a0<0>(t1));
+        m[4] = lds_read_asm(T.a2<2>(t3));
+        m[5] = lds_read_asm(T.a3<3>(t0));
+        m[6] = lds_read_asm(T.a1<1>(t3));
+        m[7] = lds_read_asm(T.a2<2>(t0));
+        m[8] = lds_read_asm(T.a3<3>(t1));
+        m[9] = lds_read_asm(T.a0<0>(t3));
+        m[10] = lds_read_asm(T.a1<1>(t0));
+        m[11] = lds_read_asm(T.a2<2>(t1));
+#pragma unroll
+        for (int i = 12; i < 16; i++) m[i] = 0u;
+    }
+    aes_pin<N>(M);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t* m = M + 16 * j;
+        g[j]->q[0] = xor3_u32(m[0], m[1], m[2]) ^ k2.x;
+        g[j]->q[1] = xor3_u32(m[3], m[4], m[5]) ^ k2.y;
+        g[j]->q[2] = xor3_u32(m[6], m[7], m[8]) ^ k2.z;
+        g[j]->q[3] = xor3_u32(m[9], m[10], m[11]) ^ k2.w;
+    }
+}
+
+// XofFixedKeyAes128 blocks j < N: counter ctr[j] of the seed of group g[j]
+// (ctr[j] >> 8 must be the group's ctr_hi >> 8), in lockstep.
+template <int N, class RK>
+MH_D void ctr_blocks_n(const AesPerm& T, const RK& rk, const AesCtrGroup* const (&g)[N],
+                       const uint32_t* const (&seed)[N], const uint32_t (&ctr)[N], uint32_t* const (&out)[N]) {
+    // round 1: the one varying lookup per block
+    uint32_t L1[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) L1[j] = lds_read_asm(g[j]->a ^ ((ctr[j] & 0xffu) << 8));
+    if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(L1[0]));
+    else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(L1[0]), "+v"(L1[1]));
+    else {
+        static_assert(N == 4, "N = 1, 2 or 4");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(L1[0]), "+v"(L1[1]), "+v"(L1[2]), "+v"(L1[3]));
+    }
+    // round 2: four lookups of round-1 column 2 per block
+    uint32_t L2[4 * N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t u2 = g[j]->p2 ^ L1[j];
+        L2[4 * j + 0] = lds_read_asm(T.a2<2>(u2));
+        L2[4 * j + 1] = lds_read_asm(T.a1<1>(u2));
+        L2[4 * j + 2] = lds_read_asm(T.a0<0>(u2));
+        L2[4 * j + 3] = lds_read_asm(T.a3<3>(u2));
+    }
+    if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(L2[0]), "+v"(L2[1]), "+v"(L2[2]), "+v"(L2[3]));
+    else if constexpr (N == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(L2[0]), "+v"(L2[1]), "+v"(L2[2]), "+v"(L2[3]), "+v"(L2[4]), "+v"(L2[5]), "+v"(L2[6]),
+                       "+v"(L2[7]));
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(L2[0]), "+v"(L2[1]), "+v"(L2[2]), "+v"(L2[3]), "+v"(L2[4]), "+v"(L2[5]), "+v"(L2[6]),
+                       "+v"(L2[7]), "+v"(L2[8]), "+v"(L2[9]), "+v"(L2[10]), "+v"(L2[11]), "+v"(L2[12]),
+                       "+v"(L2[13]), "+v"(L2[14]), "+v"(L2[15]));
+    uint32_t x[N][4];
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[j][c] = g[j]->q[c] ^ L2[4 * j + c];
+#pragma unroll
+    for (int r = 3; r < 10; r++) aes_round_n<N>(T, x, rk(r));
+    aes_last_n<N>(T, x, rk(10));
+    // output: AES(sigma) ^ sigma
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const uint32_t* sd = seed[j];
+        out[j][0] = x[j][0] ^ sd[2];
+        out[j][1] = x[j][1] ^ sd[3];
+        out[j][2] = xor3_u32(x[j][2], sd[2] ^ sd[0], ctr[j]);
+        out[j][3] = xor3_u32(x[j][3], sd[3], sd[1]);
+    }
+}
+
 // XofFixedKeyAes128 blocks (seed[j], ctr[j]) for j < N, in lockstep.
 template <int N, class RK>
 MH_D void fixed_key_block_n(const AesPerm& T, const RK& rk, const uint32_t* const (&seed)[N],

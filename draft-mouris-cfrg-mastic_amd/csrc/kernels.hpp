@@ -538,6 +538,11 @@ struct AesArgs {
 // ds_read_b128 per round) are shared by all 16 waves: 86 KiB per workgroup,
 // one workgroup = 4 waves per SIMD per CU.
 #define EVAL_WAVES 16
+// Counter groups (aes.hpp): rounds 1-2 shared by the blocks of one seed in
+// the extend pair, the convert seeds and the payload fast path.
+#ifndef MASTIC_CTR_GROUPS
+#define MASTIC_CTR_GROUPS 1
+#endif
 #define EVAL_PROOF_WAVES 8  // default split (mastic_ctx::proof_waves); measured best of 2..12
 // VGPR cap of the level kernel: 4 waves x 96 per SIMD leave 128 of the 512
 // for one binder-sponge wave (k_absorb_pair), so the two kernels can share a
@@ -682,7 +687,23 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         // extend: block 0 -> left child, block 1 -> right child (one paired
         // AES call), correct, then both children's convert seed blocks.
         uint32_t cs0[4], cs1[4], ns0[4], ns1[4];
+#if MASTIC_CTR_GROUPS
+        {
+            // both extend blocks share the parent seed (aes.hpp counter groups)
+            AesCtrGroup gp;
+            const uint32_t* const sd[1] = {ps};
+            const uint32_t ch[1] = {0u};
+            AesCtrGroup* const gi[1] = {&gp};
+            ctr_group_init<1>(TL, rke, sd, ch, gi);
+            const AesCtrGroup* const gg[2] = {&gp, &gp};
+            const uint32_t* const sd2[2] = {ps, ps};
+            const uint32_t cv[2] = {0u, 1u};
+            uint32_t* const ov[2] = {cs0, cs1};
+            ctr_blocks_n<2>(TL, rke, gg, sd2, cv, ov);
+        }
+#else
         fixed_key_block2(TL, rke, ps, 0u, ps, 1u, cs0, cs1);
+#endif
         uint32_t tc0 = cs0[0] & 1u, tc1 = cs1[0] & 1u;
         cs0[0] &= ~1u;
         cs1[0] &= ~1u;
@@ -695,7 +716,28 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             tc0 ^= ccw & 1u;
             tc1 ^= (ccw >> 1) & 1u;
         }
+#if MASTIC_CTR_GROUPS
+        // each child's convert stream (next seed: counter 0, payload blocks:
+        // counters 1, 2, ...) is one counter group per 256 counters
+        AesCtrGroup g0, g1;
+        uint32_t g_hi = 0;  // counter bits above 7 of the groups (uniform)
+        const uint32_t* const csd[2] = {cs0, cs1};
+        auto init_groups = [&](uint32_t hi) {
+            const uint32_t ch2[2] = {hi, hi};
+            AesCtrGroup* const gi[2] = {&g0, &g1};
+            ctr_group_init<2>(TL, rkc, csd, ch2, gi);
+            g_hi = hi;
+        };
+        const AesCtrGroup* const gg[2] = {&g0, &g1};
+        init_groups(0u);
+        {
+            const uint32_t cv[2] = {0u, 0u};
+            uint32_t* const ov[2] = {ns0, ns1};
+            ctr_blocks_n<2>(TL, rkc, gg, csd, cv, ov);
+        }
+#else
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
+#endif
         if (ch == 0) {
             const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
 #pragma unroll
@@ -787,7 +829,17 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                     wpb = load_wp(e1);
                 }
                 uint32_t o0[4], o1[4];
+#if MASTIC_CTR_GROUPS
+                {
+                    const uint32_t c = (uint32_t)(b + 1);
+                    if ((c & ~0xffu) != g_hi) init_groups(c & ~0xffu);
+                    const uint32_t cv[2] = {c, c};
+                    uint32_t* const ov[2] = {o0, o1};
+                    ctr_blocks_n<2>(TL, rkc, gg, csd, cv, ov);
+                }
+#else
                 fixed_key_block2(TL, rkc, cs0, (uint32_t)(b + 1), cs1, (uint32_t)(b + 1), o0, o1);
+#endif
                 bool sus;
                 if constexpr (EPB == 2)
                     sus = (o0[1] == ~0u) | (o1[1] == ~0u) | (two & ((o0[3] == ~0u) | (o1[3] == ~0u)));
