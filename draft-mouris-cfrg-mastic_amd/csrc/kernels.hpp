@@ -968,6 +968,7 @@ struct AbsorbArgs {
     int nbytes[2];
     int f[2];
     int prio;  // s_setprio of the sponge waves (0..3)
+    int dbg;   // timing experiments only (results wrong): 1 no loads, 2 no permutations, 3 rolled permutation
 };
 MH_D void absorb_setprio(int prio) {
     switch (prio) {
@@ -1127,7 +1128,12 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     // before the XOR would make its wait drain them too and expose the whole
     // memory latency once per block).
     uint32_t cur[NL];
-    load_block(0, cur);
+    if (a.dbg == 1) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) cur[k] = lt + k;
+    } else {
+        load_block(0, cur);
+    }
     for (int b = 0;; b++) {
         const bool full = end >= KECCAK_RATE * (b + 1);
         const bool more = end > KECCAK_RATE * (b + 1);
@@ -1135,8 +1141,9 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
         for (int i = 0; i < 21; i++) s.a[i] ^= __builtin_amdgcn_alignbit(cur[2 * i + 1], cur[2 * i], amt);
         if (!full) break;
         asm volatile("" ::: "memory");
-        if (more) load_block(b + 1, cur);
-        keccak_p12_pair(s, h != 0);
+        if (more && a.dbg != 1) load_block(b + 1, cur);
+        if (a.dbg == 0 || a.dbg == 1) keccak_p12_pair(s, h != 0);
+        else if (a.dbg == 3) keccak_p12_pair<2>(s, h != 0);
         if (!more) break;
     }
 #pragma unroll

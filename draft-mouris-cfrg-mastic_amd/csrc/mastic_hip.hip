@@ -182,12 +182,13 @@ struct mastic_ctx {
     int proof_waves = EVAL_PROOF_WAVES;  // proof waves per eval workgroup (MASTIC_PROOF_WAVES)
     int proof_prio = 0;                  // their s_setprio (MASTIC_PROOF_PRIO)
     int aes_prio = 0;                    // s_setprio of the AES waves (MASTIC_AES_PRIO)
-    int dbg_skip = 0;                    // timing experiments only (MASTIC_DBG_SKIP; results wrong)
+    int dbg_skip = 0;                    // timing experiments only (MASTIC_DBG_SKIP; results wrong): 1 no node proofs, 2 no AES, 4 no binder sponges
     int stride_pad = 64;                 // words of padding per plane row (MASTIC_STRIDE_PAD)
     size_t work_arena = (size_t)48 << 30;  // minimum size of a new work buffer (MASTIC_WORK_ARENA_GB)
     bool binder_tiled = true;            // tiled level binder buffers (MASTIC_BINDER_TILED=0: planes)
     int absorb_threads = 256;            // threads per binder-sponge workgroup (MASTIC_ABSORB_THREADS)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
+    int absorb_dbg = 0;                  // timing experiments only (MASTIC_ABSORB_DBG, kernels.hpp AbsorbArgs::dbg)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
@@ -754,9 +755,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         ab.nbytes[1] = lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
         ab.f[1] = f_pl;
         ab.prio = c->absorb_prio;
+        ab.dbg = c->absorb_dbg;
         HIPCHK(c, hipStreamWaitEvent(c->stream2, ready, 0));
         HIPCHK(c, hipEventRecord(e4, c->stream2));
-        if (c->absorb_pair)
+        if (c->dbg_skip & 4) {
+            // timing experiments only: no binder sponges (results wrong)
+        } else if (c->absorb_pair)
             hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, 2),
                                dim3(c->absorb_threads), c->absorb_lds, c->stream2, pl, ab);
         else
@@ -1749,6 +1753,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (at) c->absorb_threads = std::max(64, std::min(256, atoi(at))) / 64 * 64;
         const char* ap = getenv("MASTIC_ABSORB_PRIO");
         if (ap) c->absorb_prio = std::max(0, std::min(3, atoi(ap)));
+        const char* adb = getenv("MASTIC_ABSORB_DBG");
+        if (adb) c->absorb_dbg = atoi(adb);
         const char* dsk = getenv("MASTIC_DBG_SKIP");
         if (dsk) c->dbg_skip = atoi(dsk);
         const char* xp = getenv("MASTIC_AES_PRIO");
