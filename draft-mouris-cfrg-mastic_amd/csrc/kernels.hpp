@@ -968,7 +968,7 @@ struct AbsorbArgs {
     int nbytes[2];
     int f[2];
     int prio;  // s_setprio of the sponge waves (0..3)
-    int dbg;   // timing experiments only (results wrong): 1 no loads, 2 no permutations, 3 rolled permutation
+    int dbg;   // timing experiments only (results wrong): 1 no loads, 2 no permutations, 4 neither (sleeps)
 };
 MH_D void absorb_setprio(int prio) {
     switch (prio) {
@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     // before the XOR would make its wait drain them too and expose the whole
     // memory latency once per block).
     uint32_t cur[NL];
-    if (a.dbg == 1) {
+    if (a.dbg == 1 || a.dbg == 4) {
 #pragma unroll
         for (int k = 0; k < NL; k++) cur[k] = lt + k;
     } else {
@@ -1141,9 +1141,9 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
         for (int i = 0; i < 21; i++) s.a[i] ^= __builtin_amdgcn_alignbit(cur[2 * i + 1], cur[2 * i], amt);
         if (!full) break;
         asm volatile("" ::: "memory");
-        if (more && a.dbg != 1) load_block(b + 1, cur);
+        if (more && a.dbg != 1 && a.dbg != 4) load_block(b + 1, cur);
         if (a.dbg == 0 || a.dbg == 1) keccak_p12_pair(s, h != 0);
-        else if (a.dbg == 3) keccak_p12_pair<2>(s, h != 0);
+        else if (a.dbg == 4) __builtin_amdgcn_s_sleep(72);  // resident, ~4.6k cycles per block, no VALU
         if (!more) break;
     }
 #pragma unroll
