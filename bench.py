@@ -494,8 +494,9 @@ def cpu_host_info():
 def main():
     args = parse()
     if args.launch_probe:  # tests: report the rank layout and exit (no GPU)
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")),
-                          "world": int(os.environ.get("WORLD_SIZE", "1")), "gpus": args.gpus}), flush=True)
+        # one write per line (atomic on a pipe): the ranks share the launcher's stdout
+        os.write(1, (json.dumps({"rank": int(os.environ.get("RANK", "0")),
+                                 "world": int(os.environ.get("WORLD_SIZE", "1")), "gpus": args.gpus}) + "\n").encode())
         return 0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

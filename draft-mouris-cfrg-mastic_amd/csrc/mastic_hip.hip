@@ -164,7 +164,7 @@ struct mastic_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // level evals, setup, finalize, FLP
     hipStream_t stream2 = nullptr;  // binder sponges (overlap the next level's eval)
-    hipStream_t stream3 = nullptr;  // node proofs (VALU-only, overlap the LDS-bound AES)
+    hipStream_t stream3 = nullptr;  // binder sponges of the odd chunks of a pipelined prep_init
     std::vector<hipEvent_t> sync_ev;
     hipEvent_t fold_ev = nullptr;  // mastic_fold_shares: producer stream -> stream
     PrefixState pfx_host[PFX_COUNT];
@@ -191,6 +191,7 @@ struct mastic_ctx {
     int absorb_dbg = 0;                  // timing experiments only (MASTIC_ABSORB_DBG, kernels.hpp AbsorbArgs::dbg)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
     bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
+    size_t chunk_max = 0;        // reports per chunk cap (0 = what fits; MASTIC_CHUNK_REPORTS)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
     int par_waves = 0;           // waves' worth of parents per level-kernel workgroup (0 = by field; MASTIC_PAR_WAVES)
     // Field128 payload elements per level-kernel work item (MASTIC_SPLIT_ELEMS;
@@ -690,7 +691,7 @@ static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst
 template <class F>
 static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
                      size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit, const uint32_t* cin_cs,
-                     const uint32_t* cin_w, uint32_t* W, hipStream_t tail, size_t sev0) {
+                     const uint32_t* cin_w, uint32_t* W, hipStream_t ss, hipStream_t tail, size_t sev0) {
     const McParams& p = c->p;
     Planes pl = make_planes(W, wl, n, stride);
     // Every level plane (child seeds, frontier payloads, proof / payload-
@@ -756,19 +757,19 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         ab.f[1] = f_pl;
         ab.prio = c->absorb_prio;
         ab.dbg = c->absorb_dbg;
-        HIPCHK(c, hipStreamWaitEvent(c->stream2, ready, 0));
-        HIPCHK(c, hipEventRecord(e4, c->stream2));
+        HIPCHK(c, hipStreamWaitEvent(ss, ready, 0));
+        HIPCHK(c, hipEventRecord(e4, ss));
         if (c->dbg_skip & 4) {
             // timing experiments only: no binder sponges (results wrong)
         } else if (c->absorb_pair)
             hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, 2),
-                               dim3(c->absorb_threads), c->absorb_lds, c->stream2, pl, ab);
+                               dim3(c->absorb_threads), c->absorb_lds, ss, pl, ab);
         else
-            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, c->stream2, pl, ab);
-        HIPCHK(c, hipEventRecord(e5, c->stream2));
+            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, ss, pl, ab);
+        HIPCHK(c, hipEventRecord(e5, ss));
         HIPCHK(c, hipGetLastError());
         abs_done[lv] = get_sync_event(c, sev++);
-        HIPCHK(c, hipEventRecord(abs_done[lv], c->stream2));
+        HIPCHK(c, hipEventRecord(abs_done[lv], ss));
         f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
         f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
         return 0;
@@ -877,8 +878,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         if (l > 0 && !hit) {
             if (launch_absorb(l - 1, aes_done, e4, e5)) return -1;
         } else {
-            HIPCHK(c, hipEventRecord(e4, c->stream2));
-            HIPCHK(c, hipEventRecord(e5, c->stream2));
+            HIPCHK(c, hipEventRecord(e4, ss));
+            HIPCHK(c, hipEventRecord(e5, ss));
         }
     }
     if (hit && c->fuse_proofs && !(p.field == 128 && p.tgroup == 1 && c->split_elems > 0 &&
@@ -925,7 +926,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipEventRecord(np_done, c->stream));
         if (launch_absorb(l, np_done, e4, e5)) return -1;
     }
-    if (tail != c->stream2) HIPCHK(c, hipStreamWaitEvent(tail, abs_done[t->L], 0));
+    if (tail != ss) HIPCHK(c, hipStreamWaitEvent(tail, abs_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
     hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl, fa, pfx);
     if (t->weight_check) {
@@ -1135,12 +1136,17 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         chunk = std::min<size_t>(round_up(n, 64), (c->work.bytes / per_report - pad) / 64 * 64);
     }
     if (c->budget) chunk = std::min(chunk, std::max<size_t>(by_budget, 64));  // an explicit budget caps chunks
+    // MASTIC_CHUNK_REPORTS caps a chunk below what fits, so a large batch runs
+    // as several pipelined chunks (the trailing sponges of one overlap the
+    // evaluation of the next) instead of one chunk with an exposed tail
+    const bool capped = c->chunk_max > 0 && round_up(c->chunk_max, 64) < chunk;
+    if (capped) chunk = round_up(c->chunk_max, 64);
     // Several chunks: pipeline them through the two halves of the work arena
     // (chunk k+1 evaluates in one half while chunk k's last sponges, finalize
     // and copies run on the sponge stream over the other).
     const size_t half_cap = c->work.bytes / 2 / per_report;  // reports (padding rows included) per half
     const bool pipe = c->chunk_pipeline && n > chunk && chunk >= 128 && half_cap >= pad + 64;
-    if (pipe) chunk = std::min(chunk / 2, half_cap - pad) / 64 * 64;
+    if (pipe) chunk = std::min(capped ? chunk : chunk / 2, half_cap - pad) / 64 * 64;
     const size_t half = c->work.bytes / 2 / 4 / 64 * 64;  // words: second half's offset
     const size_t nsev = 2 * (size_t)t->L + 8;           // sync events one chunk uses
     size_t evi = 0;
@@ -1154,23 +1160,29 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         const int h = pipe ? (int)(k & 1) : 0;
         if (pipe && k >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, half_free[h], 0));
         uint32_t* W = c->work.as<uint32_t>() + h * half;
-        hipStream_t tail = pipe ? c->stream2 : c->stream;
+        // pipelined chunks alternate between two sponge streams: a chunk's
+        // sponges must not queue behind the previous chunk's trailing ones
+        hipStream_t ss = (pipe && h) ? c->stream3 : c->stream2;
+        hipStream_t tail = pipe ? ss : c->stream;
         rc = p.field == 64
-                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, tail, h * nsev)
-                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, tail,
+                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, ss, tail,
+                                  h * nsev)
+                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, ss, tail,
                                    h * nsev);
         if (rc) {
             for (void* q : retire_after) c->graveyard.push_back(q);
             if (lc) lc->drop();
             return rc;
         }
-        if (pipe) HIPCHK(c, hipEventRecord(half_free[h], c->stream2));
+        if (pipe) HIPCHK(c, hipEventRecord(half_free[h], ss));
     }
     if (pipe) {
         // later work on the main stream (results, aggregate, the next call) sees every chunk's tail
-        hipEvent_t done = get_sync_event(c, 2 * nsev + 2);
+        hipEvent_t done = get_sync_event(c, 2 * nsev + 2), done3 = get_sync_event(c, 2 * nsev + 3);
         HIPCHK(c, hipEventRecord(done, c->stream2));
+        HIPCHK(c, hipEventRecord(done3, c->stream3));
         HIPCHK(c, hipStreamWaitEvent(c->stream, done, 0));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, done3, 0));
     }
     for (void* q : retire_after) c->graveyard.push_back(q);
     if (lc) {
@@ -1769,6 +1781,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (cp) c->chunk_pipeline = cp[0] != '0';
         const char* fp = getenv("MASTIC_FUSE_PROOFS");
         if (fp) c->fuse_proofs = fp[0] != '0';
+        const char* cr = getenv("MASTIC_CHUNK_REPORTS");
+        if (cr) c->chunk_max = (size_t)std::max(0, atoi(cr));
         const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
         c->force_slow_blk = fs ? atoi(fs) : -1;
     }
@@ -1793,7 +1807,7 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         delete c;
         return MASTIC_EHIP;
     }
@@ -1821,6 +1835,7 @@ extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
             // queued kernels may still read the cache buffers
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamSynchronize(c->stream2);
+            (void)hipStreamSynchronize(c->stream3);
         }
         if (!on) {
             for (auto& x : c->lc) x.release();
