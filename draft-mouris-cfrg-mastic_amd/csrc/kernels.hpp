@@ -490,12 +490,16 @@ struct AesArgs {
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
     int force_slow_blk;  // test hook: the Field64 fast path hands over to the exact stream at this block (-1 = never)
-    // frontier cache (mastic_set_frontier_cache): payloads of ALL children of this level by child
-    // node index (the last level of a prep_init, read back as the parents' payloads next call), and
-    // fr_w_in indexed by the parent's node index (parent_node) instead of its ordinal
-    uint32_t* last_w;
-    int wp_by_node;
-    int in_stride;  // plane stride of cs_in / fr_w_in (the cache's, on a hit; else the work buffer's)
+    // frontier cache (mastic_set_frontier_cache).  Last level of a prep_init: the convert seeds of
+    // ALL children (extend output after correction, the seed of convert) by child node index,
+    // staged for the cache.  Cache hit: the parents' payloads are recomputed from their cached
+    // convert seeds (cv_in, by node index, plus the control bit in cs_in) into wp_buf (by parent
+    // ordinal) instead of being cached: 16 B per node instead of VALUE_LEN field elements.
+    uint32_t* last_cv;
+    const uint32_t* cv_in;
+    uint32_t* wp_buf;
+    int recompute_wp;
+    int in_stride;  // plane stride of cs_in / cv_in (the cache's, on a hit; else the work buffer's)
     // frontier-cache hit (FC only): the AES waves also compute THIS level's
     // node proofs right after each parent's payloads (no k_node_proof launch)
     int fuse_proofs;
@@ -527,6 +531,81 @@ struct AesArgs {
     int aes_prio;                   // s_setprio of the AES waves
     int dbg_skip;                   // timing experiments only (results wrong): 1 = no proof work, 2 = no AES work
 };
+
+// Frontier-cache hit: the payload w_p of a parent (a node of the cached
+// level), elements [e_lo, e_hi), recomputed from its convert seed cv and
+// control bit t exactly as its own evaluation produced it (vidpf.py:352-364
+// then the payload correction of eval_next, vidpf.py:317-319) and stored as
+// element row0 + e of the planes `out`.  Fast path: consecutive blocks of the
+// one stream in pairs (counters c, c+1 share their rounds 1-2 when c >> 8
+// agrees), speculating that no candidate is rejected; if a lane of the wave
+// meets a candidate >= p among the elements it uses, the exact next_vec
+// stream takes over from that element.
+template <class F>
+MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[4], uint32_t t, const uint32_t* cw,
+                         int S, int r, int e_lo, int e_hi, uint32_t* out, int row0) {
+    typedef typename F::E E;
+    constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
+    const int nblk = (e_hi + EPB - 1) / EPB;
+    AesCtrGroup g;
+    uint32_t g_hi = ~0u;
+    int e_fast = e_lo;
+    auto put = [&](int e, E x) {
+        if (t) x = F::add(x, pl_load<F>(cw, e, S, r));
+        pl_store<F>(out, row0 + e, S, r, x);
+    };
+    for (int b = e_lo / EPB; b < nblk; b += 2) {
+        asm volatile("" ::: "memory");
+        const uint32_t c0 = (uint32_t)(b + 1), c1 = c0 + 1;
+        const bool two = b + 1 < nblk;
+        uint32_t o[2][4];
+        if ((c0 & ~0xffu) == (c1 & ~0xffu)) {
+            if ((c0 & ~0xffu) != g_hi) {
+                const uint32_t* const sd[1] = {cv};
+                const uint32_t hv[1] = {c0 & ~0xffu};
+                AesCtrGroup* const gi[1] = {&g};
+                ctr_group_init<1>(TL, rkc, sd, hv, gi);
+                g_hi = c0 & ~0xffu;
+            }
+            const AesCtrGroup* const gg[2] = {&g, &g};
+            const uint32_t* const sd2[2] = {cv, cv};
+            const uint32_t cvv[2] = {c0, c1};
+            uint32_t* const ov[2] = {o[0], o[1]};
+            ctr_blocks_n<2>(TL, rkc, gg, sd2, cvv, ov);
+        } else {  // the pair straddles a counter group (C5's long streams)
+            const uint32_t* const sd2[2] = {cv, cv};
+            const uint32_t cvv[2] = {c0, c1};
+            uint32_t* const ov[2] = {o[0], o[1]};
+            fixed_key_block_n<2>(TL, rkc, sd2, cvv, ov);
+        }
+        // candidates of these blocks that the parent uses: elements EPB*b ..
+        bool sus = false;
+        const int e0 = EPB * b;
+#pragma unroll
+        for (int k = 0; k < 2 * EPB; k++) {
+            const int e = e0 + k;
+            const uint32_t top = EPB == 2 ? o[k >> 1][2 * (k & 1) + 1] : o[k][3];
+            if (e < e_hi && (k < EPB || two)) sus |= top == ~0u;
+        }
+        if (__builtin_expect(__any(sus), 0)) break;
+#pragma unroll
+        for (int k = 0; k < 2 * EPB; k++) {
+            const int e = e0 + k;
+            if (e < e_hi && (k < EPB || two)) put(e, F::from_words(&o[k / EPB][(k % EPB) * F::W32]));
+        }
+        e_fast = min(e_hi, e0 + 2 * EPB);
+    }
+    if (e_fast < e_hi) {
+        // exact next_vec stream from the stream's start, emitting from e_fast on
+        typename EvalStream<F, false>::type st;
+        st.init(cv);
+        for (int e = 0; e < e_hi; e++) {
+            asm volatile("" ::: "memory");
+            const E x = st.next(TL, rkc);
+            if (e >= e_fast) put(e, x);
+        }
+    }
+}
 
 // One workgroup = 64 reports (one per lane) x 16 waves: 8 AES waves walk
 // this level's parents and 8 proof waves first compute the node proofs of the
@@ -684,6 +763,19 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             nxt = rbeg < wp1 ? rbeg : -1;
         }
         if (nxt >= 0) load_parent(nxt, nps, npctrl);
+        if constexpr (FC) {
+            if (a.recompute_wp) {
+                // frontier-cache hit: this parent's payload from its cached convert seed
+                const int pn = a.parent_node[pi];
+                uint32_t pcv[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) pcv[i] = pld(a.cv_in + ((size_t)pn * 4 + i) * S_in, lb);
+                parent_payload<F>(TL, rkc, pcv, pctrl, pl.cw_w + (size_t)(l - 1) * wl * S, S, r, e_lo, e_hi, a.wp_buf,
+                                  pi * vl);
+                // the children's loop below reads these elements back (same lanes)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
         // extend: block 0 -> left child, block 1 -> right child (one paired
         // AES call), correct, then both children's convert seed blocks.
         uint32_t cs0[4], cs1[4], ns0[4], ns1[4];
@@ -738,6 +830,17 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 #else
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
 #endif
+        if constexpr (FC) {
+            if (a.last_cv && ch == 0) {
+                // convert seeds of the last level's children, staged for the frontier cache
+                const size_t n0 = (size_t)(2 * pi) * 4, n1 = n0 + 4;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    pst(a.last_cv + (n0 + i) * S, lb, cs0[i]);
+                    pst(a.last_cv + (n1 + i) * S, lb, cs1[i]);
+                }
+            }
+        }
         if (ch == 0) {
             const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
 #pragma unroll
@@ -760,12 +863,6 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             if (tc1) x1 = F::add(x1, cw);
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
-            if constexpr (FC) {
-                if (a.last_w) {
-                    pl_store<F>(a.last_w, (2 * pi) * vl + e, S, r, x0);
-                    pl_store<F>(a.last_w, (2 * pi + 1) * vl + e, S, r, x1);
-                }
-            }
             if (l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
@@ -801,9 +898,9 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             }
         };
         auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
-        int wpi = pi;
-        if constexpr (FC) wpi = a.wp_by_node ? a.parent_node[pi] : pi;
-        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(a.fr_w_in, wpi * vl + e, S_in, r) : F::zero(); };
+        const uint32_t* wpb = a.fr_w_in;
+        if constexpr (FC) wpb = a.recompute_wp ? a.wp_buf : a.fr_w_in;
+        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(wpb, pi * vl + e, S, r) : F::zero(); };
         int e_fast = e_lo;  // elements completed by the fast path
         if constexpr (!QUAD) {
             // Fast path: block b (counter b + 1) of each child's convert stream

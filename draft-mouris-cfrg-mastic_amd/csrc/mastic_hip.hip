@@ -131,15 +131,15 @@ struct LevelCache {
     std::vector<int> n_parents;                 // per level 0..L
     std::vector<uint32_t> paths;                // child paths of level L (8 words per node)
     DevBuf sp, rootsum;                         // both binder sponges (2 x 50 planes); root sum (wl planes)
-    DevBuf cs, w;                               // last level: seeds / ctrl [node][5], payloads [node][wl]
-    size_t nodes_cap = 0;                       // nodes cs / w can hold
+    DevBuf cs, cv;                              // last level: seeds / ctrl [node][5], convert seeds [node][4]
+    size_t nodes_cap = 0;                       // nodes cs / cv can hold
     void drop() { valid = false; }
     void release() {
         drop();
         sp.release();
         rootsum.release();
         cs.release();
-        w.release();
+        cv.release();
         nodes_cap = 0;
         S = 0;
     }
@@ -540,12 +540,12 @@ struct WorkLayout {
     size_t words = 0;  // per report (plane count)
     size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
         rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, cs[2], fr_w[2], onehot[3],
-        payload[3], out, lastw;
+        payload[3], out, lastcv;
 };
 static constexpr int NSLOT = 3;  // level buffers in flight between eval and absorb
 
-// cache: the frontier cache is on (the last level's payloads of every node
-// are staged in the work buffer before they are copied into the cache)
+// cache: the frontier cache is on (the last level's convert seeds of every
+// node are staged in the work buffer before they are copied into the cache)
 static WorkLayout work_layout(const McParams& p, const Tree* t, bool cache = false) {
     WorkLayout w;
     size_t o = 0;
@@ -587,7 +587,7 @@ static WorkLayout work_layout(const McParams& p, const Tree* t, bool cache = fal
         w.payload[k] = take((size_t)t->max_parents * wl);
     }
     w.out = take((size_t)std::max(t->n_prefixes, 1) * (1 + p.output_len) * p.w32);
-    w.lastw = take(cache ? (size_t)2 * t->n_parents[t->L] * wl : 0);
+    w.lastcv = take(cache ? (size_t)2 * t->n_parents[t->L] * 4 : 0);
     w.words = o;
     return w;
 }
@@ -691,7 +691,7 @@ static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst
 template <class F>
 static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
                      size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit, const uint32_t* cin_cs,
-                     const uint32_t* cin_w, uint32_t* W, hipStream_t ss, hipStream_t tail, size_t sev0) {
+                     const uint32_t* cin_cv, uint32_t* W, hipStream_t ss, hipStream_t tail, size_t sev0) {
     const McParams& p = c->p;
     Planes pl = make_planes(W, wl, n, stride);
     // Every level plane (child seeds, frontier payloads, proof / payload-
@@ -712,7 +712,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const PrefixState* pfx = (const PrefixState*)c->pfx.p;
     hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
                        rep->nonces.as<uint8_t>() + 16 * base, rep->pub.as<uint8_t>() + ps * base, ins + is * base,
-                       hit ? t->L : 0, t->L + 1);
+                       hit ? t->L - 1 : 0, t->L + 1);  // a hit recomputes level L-1's payloads: its CW
     hipLaunchKernelGGL(k_setup, dim3((stride + 255) / 256), dim3(256), 0, c->stream, pl, pfx);
     HIPCHK(c, hipGetLastError());
 
@@ -828,14 +828,19 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
         a.cs_in = hit ? cin_cs + base : plane(wl.cs[(l + 1) & 1]);
         a.cs_out = plane(wl.cs[l & 1]);
-        a.fr_w_in = hit ? cin_w + base : plane(wl.fr_w[(l + 1) & 1]);
+        a.fr_w_in = plane(wl.fr_w[(l + 1) & 1]);
         a.in_stride = hit ? (int)lc->S : stride;
         a.fr_w_out = plane(wl.fr_w[l & 1]);
         a.payload = pay_buf(l);
         a.out = plane(wl.out);
         a.force_slow_blk = c->force_slow_blk;
-        a.last_w = (lc && l == t->L) ? plane(wl.lastw) : nullptr;
-        a.wp_by_node = hit ? 1 : 0;
+        // frontier cache: stage this level's convert seeds (last level); on a
+        // hit recompute the parents' payloads from the cached ones into the
+        // (otherwise unused) parent-payload planes
+        a.last_cv = (lc && l == t->L) ? plane(wl.lastcv) : nullptr;
+        a.cv_in = hit ? cin_cv + base : nullptr;
+        a.wp_buf = plane(wl.fr_w[(l + 1) & 1]);
+        a.recompute_wp = hit ? 1 : 0;
         const bool fuse = hit && c->fuse_proofs && l == t->L && a.n_split == 1;
         a.fuse_proofs = fuse ? 1 : 0;
         a.cur_path_bytes = (l + 1 + 7) / 8;
@@ -937,11 +942,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     }
     HIPCHK(c, hipGetLastError());
     if (lc) {
-        // frontier cache for the next level: last level's seeds/ctrl and payloads, root sum.
+        // frontier cache for the next level: last level's seeds/ctrl and convert seeds, root sum.
         // Stream order: this chunk's level kernel has read its parents from the slot.
         const size_t nl = (size_t)2 * t->n_parents[t->L];
         if (to_cache(lc->cs.as<uint32_t>(), plane(wl.cs[t->L & 1]), nl * 5)) return -1;
-        if (to_cache(lc->w.as<uint32_t>(), plane(wl.lastw), nl * wlw)) return -1;
+        if (to_cache(lc->cv.as<uint32_t>(), plane(wl.lastcv), nl * 4)) return -1;
         if (!hit && to_cache(lc->rootsum.as<uint32_t>(), pl.rootsum, (size_t)wlw)) return -1;
         // both sponges after levels 0..L (stream waited for abs_done[L] above)
         if (to_cache(lc->sp.as<uint32_t>(), pl.sp_onehot, 50)) return -1;
@@ -1000,10 +1005,22 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     R.weight_check = t->weight_check;
     R.n_prefixes = t->n_prefixes;
     const size_t S = R.stride;
-    if (!R.eval_proof.grow(S * 8 * 4) || !R.status.grow(S * 4) ||
-        !R.out.grow(S * 4 * std::max<size_t>(1, (size_t)t->n_prefixes * (1 + p.output_len) * p.w32)) ||
-        !R.verifier.grow(S * 4 * (size_t)p.verifier_len * p.w32) || !R.jr_part.grow(S * 32) ||
-        !R.jr_seed.grow(S * 32))
+    // a result buffer that must grow retires the old one to the graveyard
+    // (freed at the next idle point) instead of freeing it here: hipFree
+    // waits for the whole device, i.e. for the other aggregator's queued call
+    auto rgrow = [&](DevBuf& d, size_t want) {
+        if (want <= d.bytes && d.p) return true;
+        const size_t old = d.bytes;
+        if (d.p && d.own) c->graveyard.push_back(d.p);
+        d.p = nullptr;
+        d.bytes = 0;
+        d.own = true;
+        return d.ensure(std::max(want, old + old / 2)) || d.ensure(want);
+    };
+    if (!rgrow(R.eval_proof, S * 8 * 4) || !rgrow(R.status, S * 4) ||
+        !rgrow(R.out, S * 4 * std::max<size_t>(1, (size_t)t->n_prefixes * (1 + p.output_len) * p.w32)) ||
+        !rgrow(R.verifier, S * 4 * (size_t)p.verifier_len * p.w32) || !rgrow(R.jr_part, S * 32) ||
+        !rgrow(R.jr_seed, S * 32))
         return fail(c, MASTIC_ENOMEM, "out of device memory (results for %zu reports)", n);
     HIPCHK(c, hipMemsetAsync(R.jr_part.p, 0, S * 32, c->stream));
     HIPCHK(c, hipMemsetAsync(R.jr_seed.p, 0, S * 32, c->stream));
@@ -1016,7 +1033,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     // the slot before the work buffer, so the HBM budget sees the cache
     LevelCache* lc = nullptr;
     bool hit = false;
-    const uint32_t *cin_cs = nullptr, *cin_w = nullptr;
+    const uint32_t *cin_cs = nullptr, *cin_cv = nullptr;
     std::vector<void*> retire_after;  // slot buffers the hit still reads
     std::vector<uint8_t> lkey(1, (uint8_t)vk_len);
     lkey.insert(lkey.end(), verify_key, verify_key + vk_len);
@@ -1042,7 +1059,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
             retire(lc->sp);
             retire(lc->rootsum);
             retire(lc->cs);
-            retire(lc->w);
+            retire(lc->cv);
             lc->nodes_cap = 0;
             lc->S = S1;
         }
@@ -1067,29 +1084,29 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
             size_t cap = std::max(nl, lc->nodes_cap + lc->nodes_cap / 4);
             size_t freeb = 0, totalb = 0;
             if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-                const size_t per_node = (5 + wlw) * S1 * 4;
+                const size_t per_node = (5 + 4) * S1 * 4;
                 cap = std::max(cap, std::min(4 * nl, freeb / 5 / per_node));
             }
-            DevBuf ncs, nw;
+            DevBuf ncs, ncv;
             if (!c->graveyard.empty()) {  // the other aggregator's retired slot: free it first
                 if (hipStreamSynchronize(c->stream) == hipSuccess) c->bury();
             }
-            ok = alloc(ncs, cap * 5 * S1 * 4) && alloc(nw, cap * wlw * S1 * 4);
+            ok = alloc(ncs, cap * 5 * S1 * 4) && alloc(ncv, cap * 4 * S1 * 4);
             if (ok) {
                 if (hit) {
                     cin_cs = lc->cs.as<uint32_t>();
-                    cin_w = lc->w.as<uint32_t>();
-                    retire_after = {lc->cs.p, lc->w.p};
-                    lc->cs.p = lc->w.p = nullptr;
-                    lc->cs.bytes = lc->w.bytes = 0;
+                    cin_cv = lc->cv.as<uint32_t>();
+                    retire_after = {lc->cs.p, lc->cv.p};
+                    lc->cs.p = lc->cv.p = nullptr;
+                    lc->cs.bytes = lc->cv.bytes = 0;
                 } else {
                     retire(lc->cs);
-                    retire(lc->w);
+                    retire(lc->cv);
                 }
                 std::swap(lc->cs.p, ncs.p);
                 std::swap(lc->cs.bytes, ncs.bytes);
-                std::swap(lc->w.p, nw.p);
-                std::swap(lc->w.bytes, nw.bytes);
+                std::swap(lc->cv.p, ncv.p);
+                std::swap(lc->cv.bytes, ncv.bytes);
                 lc->nodes_cap = cap;
             }
         }
@@ -1101,7 +1118,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
             hit = false;
         } else if (hit && !cin_cs) {
             cin_cs = lc->cs.as<uint32_t>();
-            cin_w = lc->w.as<uint32_t>();
+            cin_cv = lc->cv.as<uint32_t>();
         }
         if (!hit && lc) lc->drop();  // refilled by this call
     } else {
@@ -1125,7 +1142,11 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     // sweep whose trees grow from level to level does not re-allocate it at
     // every level.
     const size_t have = c->work.bytes / per_report;
-    if (have >= std::min(chunk, round_up(n, 64)) + pad) {
+    // An arena that holds half the batch in chunks of >= 64k reports is used
+    // as it is (pipelined chunks of that size keep the GPU full and hide each
+    // other's sponge tails) rather than re-allocated for a single chunk.
+    const size_t need = std::min(chunk, round_up(n, 64)) + pad;
+    if (have >= need || (2 * have >= need && have >= pad + 2 * 65536)) {
         chunk = std::min<size_t>(round_up(n, 64), (have - pad) / 64 * 64);
     } else {
         if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
@@ -1165,9 +1186,9 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         hipStream_t ss = (pipe && h) ? c->stream3 : c->stream2;
         hipStream_t tail = pipe ? ss : c->stream;
         rc = p.field == 64
-                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, ss, tail,
+                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_cv, W, ss, tail,
                                   h * nsev)
-                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_w, W, ss, tail,
+                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_cv, W, ss, tail,
                                    h * nsev);
         if (rc) {
             for (void* q : retire_after) c->graveyard.push_back(q);
@@ -1658,7 +1679,11 @@ static int shard_impl(mastic_ctx* c, mastic_reports* rep, const uint8_t* alphas,
                          2 * (size_t)p.arity * p.P * p.w32 + 2 * (size_t)p.proof_len * p.w32 + 32;
     const uint64_t budget = default_budget(c);
     size_t chunk = std::min<size_t>(round_up(n, 64), std::max<size_t>(64, (budget / (words * 4)) / 64 * 64));
-    DevBuf scratch;
+    // the scratch is the ctx's work arena (kept across calls, stream-ordered
+    // after earlier prep_inits): sharding a large batch leaves the arena that
+    // its prep_inits then reuse instead of freeing it and allocating again
+    // (large hipMallocs / hipFrees cost ~1 s per 50-100 GB on MI355X)
+    DevBuf& scratch = c->work;
     if (!scratch.ensure(words * 4 * chunk)) return fail(c, MASTIC_ENOMEM, "out of device memory (shard scratch)");
     for (size_t b = 0; b < n; b += chunk) {
         const int nn = (int)std::min(chunk, n - b);
