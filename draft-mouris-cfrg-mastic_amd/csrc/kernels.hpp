@@ -543,7 +543,7 @@ struct AesArgs {
 // stream takes over from that element.
 template <class F>
 MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[4], uint32_t t, const uint32_t* cw,
-                         int S, int r, int e_lo, int e_hi, uint32_t* out, int row0) {
+                         int S, int r, int e_lo, int e_hi, uint32_t* out, int row0, int force_slow_blk) {
     typedef typename F::E E;
     constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
     const int nblk = (e_hi + EPB - 1) / EPB;
@@ -587,7 +587,7 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
             const uint32_t top = EPB == 2 ? o[k >> 1][2 * (k & 1) + 1] : o[k][3];
             if (e < e_hi && (k < EPB || two)) sus |= top == ~0u;
         }
-        if (__builtin_expect(__any(sus), 0)) break;
+        if (__builtin_expect(__any(sus), 0) || b == force_slow_blk || b + 1 == force_slow_blk) break;
 #pragma unroll
         for (int k = 0; k < 2 * EPB; k++) {
             const int e = e0 + k;
@@ -771,7 +771,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; i++) pcv[i] = pld(a.cv_in + ((size_t)pn * 4 + i) * S_in, lb);
                 parent_payload<F>(TL, rkc, pcv, pctrl, pl.cw_w + (size_t)(l - 1) * wl * S, S, r, e_lo, e_hi, a.wp_buf,
-                                  pi * vl);
+                                  pi * vl, a.force_slow_blk);
                 // the children's loop below reads these elements back (same lanes)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }

@@ -102,3 +102,53 @@ def test_gpu_matches_rejection_fixture(name):
         for (i, w) in enumerate(p["reports"]):
             if w["prep_msg"]:
                 assert msgs[32 * i:32 * (i + 1)].hex() == w["prep_msg"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("force_slow", [None, 0, 3])
+@pytest.mark.parametrize("name", FIXTURES)
+def test_gpu_cache_hit_recomputes_rejected_parent(name, force_slow, monkeypatch):
+    """Frontier-cache hit over the fixture's rejected node: at level 1 both
+    level-0 nodes are parents, and the cached call recomputes each parent's
+    payload from its cached convert seed -- for report B through the real
+    rejection (the exact next_vec stream), and with MASTIC_FORCE_SLOW_BLK
+    through a forced handover at a payload block.  Prep shares and out shares
+    of the hit equal a context without the cache and the oracle."""
+    import mastic_amd
+    if force_slow is not None:
+        monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(force_slow))
+    fx = _load(name)
+
+    def mk():
+        if fx["circuit"] == "MasticSum":
+            return mastic_amd.MasticSum(fx["bits"], 255)
+        return mastic_amd.MasticHistogram(fx["bits"], 64, 8)
+    m_on, m_off = mk(), mk()
+    m_on.set_frontier_cache(True)
+    o = _oracle(fx)
+    ctx, nonce = bytes.fromhex(fx["ctx"]), bytes.fromhex(fx["nonce"])
+    reps = fx["reports"]
+    n = len(reps)
+    pub = bytes.fromhex("".join(r["public_share"] for r in reps))
+    ins = [bytes.fromhex("".join(r["input_shares"][a] for r in reps)) for a in range(2)]
+    dev_on = m_on.reports_upload(nonce * n, pub, ins[0], ins[1])
+    dev_off = m_off.reports_upload(nonce * n, pub, ins[0], ins[1])
+    vk = bytes.fromhex(fx["verify_key"])
+    F, T = False, True
+    ap0 = (0, ((F,), (T,)), False)
+    ap1 = (1, ((F, F), (F, T), (T, F), (T, T)), False)
+    for agg_id in range(2):
+        for ap in (ap0, ap1):
+            m_on.prep_init_device(dev_on, vk, ctx, agg_id, ap)
+            m_off.prep_init_device(dev_off, vk, ctx, agg_id, ap)
+            a = m_on.prep_result(dev_on, agg_id, ap, want_out_shares=True)
+            b = m_off.prep_result(dev_off, agg_id, ap, want_out_shares=True)
+            if ap is ap1:
+                assert m_on.last_prep_was_cached(), "level 1 should extend the cached level-0 tree"
+            assert a[0] == b[0] and a[2] == b[2], (ap[0], agg_id)
+            psz = len(a[0]) // n
+            for (i, r) in enumerate(reps):
+                cws = o.vidpf.decode_public_share(bytes.fromhex(r["public_share"]))
+                isd = o.decode_input_share(agg_id, bytes.fromhex(r["input_shares"][agg_id]))
+                (_st, sh) = o.prep_init(vk, ctx, agg_id, ap, nonce, cws, isd)
+                assert a[0][psz * i:psz * (i + 1)] == o.test_vec_encode_prep_share(sh), (ap[0], agg_id, i)
