@@ -170,10 +170,11 @@ int mastic_proof_tree(mastic_ctx* ctx, int agg_id, const uint8_t* app_ctx, size_
  * examples.py:37-91 re-evaluates the whole tree at every level).  on = 1
  * enables it, 0 disables it and frees its buffers, -1 leaves it unchanged.
  * With it on, prep_init keeps per report the two binder sponges' states
- * (400 B) plus the last level's seeds and payloads; a later prep_init for the
- * same reports, agg_id, verify key and ctx whose tree is the cached tree plus
- * one level (the sweep with no candidate path pruned away) evaluates only that
- * level and resumes the sponges from the cached states (the binder messages
+ * (400 B) plus the last level's seeds, control bits and convert seeds; a
+ * later prep_init for the same reports, agg_id, verify key and ctx whose tree
+ * is the cached tree plus one level (the sweep with no candidate path pruned
+ * away) recomputes its parents' payloads from their convert seeds, evaluates
+ * only that level and resumes the sponges from the cached states (the binder messages
  * are BFS-ordered, so the cached ones are prefixes of the new ones).  Results
  * are identical either way.  *last_hit (if not NULL) = 1 when the last
  * prep_init took the cached path. */
