@@ -868,7 +868,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
         hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
         HIPCHK(c, hipEventRecord(e0, c->stream));
-        if (lc)
+        // the frontier-cache variant only where its features are used: the
+        // last level (convert seeds staged for the cache) and a hit (parent
+        // payloads recomputed, fused proofs); a miss's other levels run the
+        // plain kernel (the variant's uniform branches and extra spills cost
+        // a few per cent)
+        if (lc && (hit || l == t->L))
             hipLaunchKernelGGL((k_eval_aes<F, false, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
                                p, pl, a);
         else
