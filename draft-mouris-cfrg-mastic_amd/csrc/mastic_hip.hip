@@ -190,7 +190,9 @@ struct mastic_ctx {
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int absorb_dbg = 0;                  // timing experiments only (MASTIC_ABSORB_DBG, kernels.hpp AbsorbArgs::dbg)
     int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
-    bool fuse_proofs = true;    // cache hits: node proofs in the level kernel (MASTIC_FUSE_PROOFS=0: k_node_proof)
+    bool fc_all = false;        // A/B only: the frontier-cache kernel variant at every level (MASTIC_FC_ALL=1)
+    int fuse_proofs = 1;        // last level's node proofs in the level kernel: 1 on cache hits, 2 also on
+                                // cache-on misses, 0 never (MASTIC_FUSE_PROOFS; else k_node_proof)
     size_t chunk_max = 0;        // reports per chunk cap (0 = what fits; MASTIC_CHUNK_REPORTS)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
     int par_waves = 0;           // waves' worth of parents per level-kernel workgroup (0 = by field; MASTIC_PAR_WAVES)
@@ -801,6 +803,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // the root sum of the cached level-0 evaluation (counter check)
         if (from_cache(pl.rootsum, lc->rootsum.as<uint32_t>(), (size_t)wlw)) return -1;
     }
+    // the last level's node proofs in the level kernel (after each workgroup's
+    // parents) instead of a k_node_proof launch: cache hits, and with
+    // MASTIC_FUSE_PROOFS=2 cache-on misses too (whole parents only)
+    const bool fuse_last = (hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs >= 2)) &&
+                           !(p.field == 128 && p.tgroup == 1 && c->split_elems > 0 && p.value_len > c->split_elems);
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
         if (!hit && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
@@ -841,7 +848,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.cv_in = hit ? cin_cv + base : nullptr;
         a.wp_buf = plane(wl.fr_w[(l + 1) & 1]);
         a.recompute_wp = hit ? 1 : 0;
-        const bool fuse = hit && c->fuse_proofs && l == t->L && a.n_split == 1;
+        const bool fuse = fuse_last && l == t->L;
         a.fuse_proofs = fuse ? 1 : 0;
         a.cur_path_bytes = (l + 1 + 7) / 8;
         a.cur_child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
@@ -873,7 +880,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // payloads recomputed, fused proofs); a miss's other levels run the
         // plain kernel (the variant's uniform branches and extra spills cost
         // a few per cent)
-        if (lc && (hit || l == t->L))
+        if (lc && (hit || l == t->L || c->fc_all))
             hipLaunchKernelGGL((k_eval_aes<F, false, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
                                p, pl, a);
         else
@@ -892,8 +899,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             HIPCHK(c, hipEventRecord(e5, ss));
         }
     }
-    if (hit && c->fuse_proofs && !(p.field == 128 && p.tgroup == 1 && c->split_elems > 0 &&
-                                  p.value_len > c->split_elems)) {
+    if (fuse_last) {
         // the last level's proofs came from the level kernel's AES waves: its sponges
         const int l = t->L;
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
@@ -1810,7 +1816,9 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         const char* cp = getenv("MASTIC_CHUNK_PIPELINE");
         if (cp) c->chunk_pipeline = cp[0] != '0';
         const char* fp = getenv("MASTIC_FUSE_PROOFS");
-        if (fp) c->fuse_proofs = fp[0] != '0';
+        if (fp) c->fuse_proofs = std::max(0, std::min(2, atoi(fp)));
+        const char* fa = getenv("MASTIC_FC_ALL");
+        if (fa) c->fc_all = fa[0] == '1';
         const char* cr = getenv("MASTIC_CHUNK_REPORTS");
         if (cr) c->chunk_max = (size_t)std::max(0, atoi(cr));
         const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
