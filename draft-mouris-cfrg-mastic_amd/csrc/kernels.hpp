@@ -619,6 +619,9 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
 #define EVAL_WAVES 16
 // Counter groups (aes.hpp): rounds 1-2 shared by the blocks of one seed in
 // the extend pair, the convert seeds and the payload fast path.
+#ifndef MASTIC_EMIT_WAIT
+#define MASTIC_EMIT_WAIT 1
+#endif
 #ifndef MASTIC_CTR_GROUPS
 #define MASTIC_CTR_GROUPS 1
 #endif
@@ -900,8 +903,16 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         auto load_cw = [&](int e) { return pl_load<F>(wcw, e, S, r); };
         const uint32_t* wpb = a.fr_w_in;
         if constexpr (FC) wpb = a.recompute_wp ? a.wp_buf : a.fr_w_in;
-        auto load_wp = [&](int e) { return l > 0 ? pl_load<F>(wpb, pi * vl + e, S, r) : F::zero(); };
+        // level 0: the root's "parent payload" planes are zeroed by the host
+        // (no branch, no zero-initialised registers in the block loop)
+        auto load_wp = [&](int e) { return pl_load<F>(wpb, pi * vl + e, S, r); };
         int e_fast = e_lo;  // elements completed by the fast path
+#if MASTIC_EMIT_WAIT
+        // the same before the block loop: the next parent's prefetched seed
+        // and this parent's child-seed stores are long done; without it the
+        // waitcnt pass keeps a vmcnt wait in the loop header (every block)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
         if constexpr (!QUAD) {
             // Fast path: block b (counter b + 1) of each child's convert stream
             // holds Field64 candidates 2b and 2b + 1, or Field128 candidate b
@@ -943,6 +954,15 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 else
                     sus = (o0[3] == ~0u) | (o1[3] == ~0u);
                 if (__builtin_expect(__any(sus), 0) || b == a.force_slow_blk) break;
+                // All of this block's loads (issued before its AES) and the
+                // previous block's stores have long completed: say so with one
+                // explicit wait.  Otherwise the waitcnt pass, which loses track
+                // of the conditionally issued loads, waits for vmcnt(2..3)
+                // between the stores below, i.e. for the stores themselves to
+                // be acknowledged, several times per block.
+#if MASTIC_EMIT_WAIT
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched
+#endif
                 emit(e, F::from_words(o0), F::from_words(o1), cwa, wpa);
                 if constexpr (EPB == 2) {
                     if (two) emit(e + 1, F::from_words(o0 + 2), F::from_words(o1 + 2), cwb, wpb);

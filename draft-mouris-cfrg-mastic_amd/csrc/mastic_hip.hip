@@ -707,8 +707,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // status plane: it clears just that.
     if (hit)
         HIPCHK(c, hipMemsetAsync(pl.status, 0, (size_t)stride * 4, c->stream));
-    else
+    else {
         HIPCHK(c, hipMemsetAsync(W, 0, wl.cs[0] * (size_t)stride * 4, c->stream));
+        // level 0 reads its parent (the root) payload from fr_w[1]: zeros
+        HIPCHK(c, hipMemsetAsync(W + wl.fr_w[1] * (size_t)stride, 0, (size_t)p.value_len * p.w32 * stride * 4, c->stream));
+    }
     const size_t ps = mc_public_share_size(p), is = mc_input_share_size(p, agg_id);
     const uint8_t* ins = agg_id == 0 ? rep->in0.as<uint8_t>() : rep->in1.as<uint8_t>();
     const PrefixState* pfx = (const PrefixState*)c->pfx.p;
