@@ -558,6 +558,11 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
         asm volatile("" ::: "memory");
         const uint32_t c0 = (uint32_t)(b + 1), c1 = c0 + 1;
         const bool two = b + 1 < nblk;
+        // this pair's payload correction words, loaded before its AES (after
+        // the previous pair's stores they would wait for those stores)
+        E cwv[2 * EPB];
+#pragma unroll
+        for (int k = 0; k < 2 * EPB; k++) cwv[k] = pl_load<F>(cw, min(EPB * b + k, e_hi - 1), S, r);
         uint32_t o[2][4];
         if ((c0 & ~0xffu) == (c1 & ~0xffu)) {
             if ((c0 & ~0xffu) != g_hi) {
@@ -588,10 +593,15 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
             if (e < e_hi && (k < EPB || two)) sus |= top == ~0u;
         }
         if (__builtin_expect(__any(sus), 0) || b == force_slow_blk || b + 1 == force_slow_blk) break;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loads above and the previous stores are done
 #pragma unroll
         for (int k = 0; k < 2 * EPB; k++) {
             const int e = e0 + k;
-            if (e < e_hi && (k < EPB || two)) put(e, F::from_words(&o[k / EPB][(k % EPB) * F::W32]));
+            if (e < e_hi && (k < EPB || two)) {
+                E x = F::from_words(&o[k / EPB][(k % EPB) * F::W32]);
+                if (t) x = F::add(x, cwv[k]);
+                pl_store<F>(out, row0 + e, S, r, x);
+            }
         }
         e_fast = min(e_hi, e0 + 2 * EPB);
     }
