@@ -102,49 +102,78 @@ struct Planes {
 };
 
 // ------------------------------------------------------------- unpack
+// nw little-endian words of one report's wire row into plane rows dst[k * step].
+// A == 8: the row, the segment and every report's row start are 8-byte aligned
+// (the common case: BITS a multiple of 32), so a lane reads two words per load
+// instead of eight byte loads (each lane reads its own row: every load of the
+// wave touches 64 cache lines, so the instruction count is what costs).
+template <int A>
+MH_D void unpack_words(const uint8_t* src, int nw, uint32_t* dst, size_t step) {
+    if constexpr (A == 8) {
+        const uint2* s2 = (const uint2*)src;
+        int k = 0;
+        for (; k + 1 < nw; k += 2) {
+            const uint2 v = s2[k >> 1];
+            dst[(size_t)k * step] = v.x;
+            dst[(size_t)(k + 1) * step] = v.y;
+        }
+        if (k < nw) dst[(size_t)k * step] = ((const uint32_t*)src)[k];
+    } else {
+        for (int k = 0; k < nw; k++) dst[(size_t)k * step] = ld_u32_bytes(src + 4 * k);
+    }
+}
+
 // Wire public share: pack_bits(ctrl) || seed_cw[B] || w_cw[B] || proof_cw[B]
 // (poc/vidpf.py:382-394).  Input share: key || [leader proof share] || [seed]
 // || [peer jr part] (poc/mastic.py:516-529).
+template <int A>
+MH_D void unpack_report(const McParams& p, const Planes& pl, int agg_id, int r, const uint8_t* ps, const uint8_t* is,
+                        const uint8_t* nc, int l_lo, int l_hi) {
+    const size_t S = (size_t)pl.stride;
+    const int nctrl = (2 * p.bits + 7) / 8;
+    const int wl = p.value_len * p.w32;
+    unpack_words<A>(nc, 4, pl.nonce + r, S);
+    unpack_words<A>(is, 4, pl.key + r, S);
+    for (int l = l_lo; l < l_hi; l++) {
+        uint32_t c0 = (ps[(2 * l) >> 3] >> ((2 * l) & 7)) & 1;
+        uint32_t c1 = (ps[(2 * l + 1) >> 3] >> ((2 * l + 1) & 7)) & 1;
+        pl.cw_ctrl[(size_t)l * S + r] = c0 | (c1 << 1);
+        unpack_words<A>(ps + nctrl + 16 * l, 4, pl.cw_seed + (size_t)l * 4 * S + r, S);
+        unpack_words<A>(ps + nctrl + 16 * p.bits + (size_t)l * p.value_len * p.enc, wl,
+                        pl.cw_w + (size_t)l * wl * S + r, S);
+        unpack_words<A>(ps + nctrl + 16 * p.bits + (size_t)p.bits * p.value_len * p.enc + 32 * l, 8,
+                        pl.cw_proof + (size_t)l * 8 * S + r, S);
+    }
+    const uint8_t* q = is + 16;
+    if (agg_id == 0) {
+        unpack_words<A>(q, p.proof_len * p.w32, pl.lps + r, S);
+        q += (size_t)p.proof_len * p.enc;
+    }
+    if (agg_id == 1 || p.joint_rand_len > 0) {
+        unpack_words<A>(q, 8, pl.seed + r, S);
+        q += 32;
+    }
+    if (p.joint_rand_len > 0) unpack_words<A>(q, 8, pl.peer + r, S);
+}
+
 __global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_id, const uint8_t* nonces,
                                                 const uint8_t* pub, const uint8_t* ins, int l_lo, int l_hi) {
     // correction words of levels l_lo .. l_hi-1 only: a call at level L never
     // reads deeper ones, and a frontier-cache hit only reads level L's
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= pl.n) return;
-    const int S = pl.stride;
     const size_t ps_size = mc_public_share_size(p);
     const size_t is_size = mc_input_share_size(p, agg_id);
     const uint8_t* ps = pub + ps_size * r;
     const uint8_t* is = ins + is_size * r;
     const uint8_t* nc = nonces + 16 * (size_t)r;
-    const int nctrl = (2 * p.bits + 7) / 8;
-    const int wl = p.value_len * p.w32;
-    for (int i = 0; i < 4; i++) {
-        pl.nonce[i * S + r] = ld_u32_bytes(nc + 4 * i);
-        pl.key[i * S + r] = ld_u32_bytes(is + 4 * i);
-    }
-    for (int l = l_lo; l < l_hi; l++) {
-        uint32_t c0 = (ps[(2 * l) >> 3] >> ((2 * l) & 7)) & 1;
-        uint32_t c1 = (ps[(2 * l + 1) >> 3] >> ((2 * l + 1) & 7)) & 1;
-        pl.cw_ctrl[(size_t)l * S + r] = c0 | (c1 << 1);
-        for (int i = 0; i < 4; i++)
-            pl.cw_seed[((size_t)l * 4 + i) * S + r] = ld_u32_bytes(ps + nctrl + 16 * l + 4 * i);
-        const uint8_t* wsrc = ps + nctrl + 16 * p.bits + (size_t)l * p.value_len * p.enc;
-        for (int k = 0; k < wl; k++) pl.cw_w[((size_t)l * wl + k) * S + r] = ld_u32_bytes(wsrc + 4 * k);
-        const uint8_t* psrc = ps + nctrl + 16 * p.bits + (size_t)p.bits * p.value_len * p.enc + 32 * l;
-        for (int i = 0; i < 8; i++) pl.cw_proof[((size_t)l * 8 + i) * S + r] = ld_u32_bytes(psrc + 4 * i);
-    }
-    const uint8_t* q = is + 16;
-    if (agg_id == 0) {
-        for (int k = 0; k < p.proof_len * p.w32; k++) pl.lps[(size_t)k * S + r] = ld_u32_bytes(q + 4 * k);
-        q += (size_t)p.proof_len * p.enc;
-    }
-    if (agg_id == 1 || p.joint_rand_len > 0) {
-        for (int i = 0; i < 8; i++) pl.seed[i * S + r] = ld_u32_bytes(q + 4 * i);
-        q += 32;
-    }
-    if (p.joint_rand_len > 0)
-        for (int i = 0; i < 8; i++) pl.peer[i * S + r] = ld_u32_bytes(q + 4 * i);
+    const size_t nctrl = (2 * p.bits + 7) / 8;
+    // every segment offset is nctrl plus multiples of 8 bytes (enc is 8 or 16)
+    const bool a8 = (((uintptr_t)pub | (uintptr_t)ins | (uintptr_t)nonces | ps_size | is_size | nctrl) & 7) == 0;
+    if (a8)
+        unpack_report<8>(p, pl, agg_id, r, ps, is, nc, l_lo, l_hi);
+    else
+        unpack_report<1>(p, pl, agg_id, r, ps, is, nc, l_lo, l_hi);
 }
 
 // ------------------------------------------------------------- key setup
