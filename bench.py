@@ -93,6 +93,15 @@ def parse():
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--frontier-cache", type=int, default=1,
                     help="sweep configs: keep each level's binder inputs in HBM (Mastic.set_frontier_cache)")
+    ap.add_argument("--split", type=int, default=0,
+                    help="sweep configs: --reports is the JOB's report count, divided over the ranks (strong "
+                         "scaling; thresholds from the job total); c2: the resident reports of the full_job leg")
+    ap.add_argument("--virtual-ranks", type=int, default=1,
+                    help="sweep configs, one GPU: time rank 0's share of a K-way split job (the other ranks' "
+                         "aggregates added in plaintext per level), to predict K-GPU strong scaling")
+    ap.add_argument("--north-star", type=int, default=1,
+                    help="c2: after the headline, the north_star job (1M-report full 32-level c2sweep, split over "
+                         "the ranks) under a north_star key; 0 skips it")
     return ap.parse_args()
 
 
@@ -183,52 +192,168 @@ def cpu_baseline(jobs, procs):
     return wall, res
 
 
-# ---------------------------------------------------------------- C3 sweep
-def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
-    """BASELINE configs C1 and C3: the reference's heavy-hitters driver
-    (examples.py:37-91, mastic_amd.heavy_hitters) over HBM-resident reports,
-    each rank sweeping its shard and merging every level's agg shares over
-    RCCL before pruning.  A step = one full level sweep (both aggregators'
-    prep_init, decide, fold and merge at every level).  Units = sum over
-    levels and aggregators of reports x candidate prefixes."""
-    from mastic_amd import Mastic
-    from mastic_amd.heavy_hitters import compute_heavy_hitters
-    from mastic_amd.merge import merge_field_shares
-
-    kw = dict(cfg["kw"])
-    bits = kw.pop("bits")
-    m = Mastic(bits, cfg["circuit"], device=local, **kw)
-    ctx = b"mastic-mi355x-bench"
-    seed = 0x4D41 + int(args.config[1])
+# ---------------------------------------------------------------- sweeps
+def sweep_population(cfg, bits, kw, seed, n, stream):
+    """Synthetic sweep reports: alphas Zipf over a pool of
+    attributes, weights per circuit, random nonces and randomness.  Returns
+    (alphas uint8 [n, ceil(bits/8)], weights int64 [n], betas, nonces, rands)."""
     if cfg.get("pool") == "c2":  # the C2 attribute set (same draws as bench --config c2)
         pool = _attrs(np.random.default_rng(seed), bits, 10000)
     else:
         pool = np.random.default_rng(seed).integers(0, 256, size=(cfg["pool"], bits // 8), dtype=np.uint8)
-    rrng = np.random.default_rng(seed * 1000003 + rank)
-    ranks = rrng.zipf(cfg["zipf"], size=n_rep)
+    rrng = np.random.default_rng(stream)
+    ranks = rrng.zipf(cfg["zipf"], size=n)
     while (ranks > len(pool)).any():
         bad = ranks > len(pool)
         ranks[bad] = rrng.zipf(cfg["zipf"], size=int(bad.sum()))
-    alpha_b = pool[ranks - 1].tobytes()
+    alphas = pool[ranks - 1]
     if cfg["circuit"] == "Sum":  # weights uniform 0..max
-        w = rrng.integers(0, kw["max_measurement"] + 1, size=n_rep)
+        w = rrng.integers(0, kw["max_measurement"] + 1, size=n)
         nb = int(kw["max_measurement"]).bit_length()
         off = 2 ** nb - 1 - kw["max_measurement"]
         betas = np.concatenate([(w[:, None] >> np.arange(nb)) & 1, ((w + off)[:, None] >> np.arange(nb)) & 1],
-                               axis=1).astype("<u8").tobytes()
-        # 0.05 % of the job's expected total weight (identical on every rank)
-        threshold = max(1, int(np.ceil(cfg["threshold_frac"] * n_rep * world * kw["max_measurement"] / 2)))
+                               axis=1).astype("<u8")
     else:
-        w = (rrng.random(n_rep) < cfg["weight_p"]).astype(np.int64)
-        threshold = cfg["threshold"] or max(1, int(np.ceil(0.0005 * n_rep * world)))
-        betas = w.astype("<u8").tobytes()
-    nonces = rrng.integers(0, 256, size=16 * n_rep, dtype=np.uint8).tobytes()
-    rands = rrng.integers(0, 256, size=m.RAND_SIZE * n_rep, dtype=np.uint8).tobytes()
-    reps = m.reports_shard(ctx, alpha_b, betas, nonces, rands)
+        w = (rrng.random(n) < cfg["weight_p"]).astype(np.int64)
+        betas = w.astype("<u8")
+    nonces = rrng.integers(0, 256, size=16 * n, dtype=np.uint8)
+    return alphas, w, betas, nonces, rrng
+
+
+def split_bounds(n_job, parts):
+    """Report ranges of a job split over `parts` ranks (strong scaling):
+    contiguous, sizes differing by at most one, covering the job."""
+    return [(n_job * i // parts, n_job * (i + 1) // parts) for i in range(parts)]
+
+
+def sweep_threshold(cfg, kw, n_job):
+    """0.05 % of the job's expected total weight (Sum) / of its reports
+    (Count), identical on every rank; C1 has a fixed threshold."""
+    if cfg["circuit"] == "Sum":
+        return max(1, int(np.ceil(cfg["threshold_frac"] * n_job * kw["max_measurement"] / 2)))
+    return cfg["threshold"] or max(1, int(np.ceil(0.0005 * n_job)))
+
+
+def prefix_sums(alphas, w, level, prefixes):
+    """Plaintext per-candidate [reports, weight] of a set of reports at a sweep
+    level (talks/func.py:49-80): the aggregate the collector unshards, as the
+    integer pairs of Count/Sum's (counter, truncated weight) output."""
+    L = level + 1
+    ab = alphas.shape[1]
+    val = np.zeros(len(alphas), dtype=np.uint64)
+    for j in range((L + 7) // 8):
+        val = (val << np.uint64(8)) | alphas[:, j].astype(np.uint64)
+    val >>= np.uint64(8 * ((L + 7) // 8) - L)
+    pv = np.array([int("".join("1" if b else "0" for b in p), 2) for p in prefixes], dtype=np.uint64)
+    order = np.argsort(pv)
+    idx = np.searchsorted(pv[order], val)
+    idx_c = np.minimum(idx, len(pv) - 1)
+    hit = pv[order][idx_c] == val
+    cnt = np.bincount(order[idx_c[hit]], minlength=len(pv))
+    ws = np.bincount(order[idx_c[hit]], weights=w[hit], minlength=len(pv))
+    del ab
+    return cnt.astype(np.int64), ws.astype(np.int64)
+
+
+class VirtualRanksMerge:
+    """One rank of a K-way split job on a single GPU (bench.py --virtual-ranks
+    K): the per-level merge adds the plaintext aggregate of the other K-1
+    ranks' reports to this rank's GPU agg shares, so the candidate trajectory,
+    and with it this rank's GPU work per level, is exactly that of rank 0 of a
+    real K-GPU run (only the RCCL all-gather of a few KB is missing).  Count
+    and Sum only (aggregate = [reports, weight] per candidate)."""
+
+    def __init__(self, m, rest_alphas, rest_w):
+        self.m = m
+        self.rest_alphas = rest_alphas
+        self.rest_w = rest_w
+        self.cur = None
+
+    def begin_level(self, level, prefixes):
+        self.cur = (level, prefixes)
+
+    def total(self, n_elems, valid=None, have_results=True):
+        import torch
+        from mastic_amd.merge import aggregate_to_tensor, fold_on_gpu
+        m = self.m
+        enc = m.field.ENCODED_SIZE
+        if n_elems == 0:
+            return b""
+        local = torch.empty(2 * n_elems * enc, dtype=torch.uint8, device="cuda")
+        for agg_id in range(2):
+            aggregate_to_tensor(m, agg_id, n_elems, valid, out=local[agg_id * n_elems * enc:])
+        merged = np.frombuffer(fold_on_gpu(m, local, 2, n_elems).cpu().numpy().tobytes(), dtype="<u8")
+        (level, prefixes) = self.cur
+        (cnt, ws) = prefix_sums(self.rest_alphas, self.rest_w, level, prefixes)
+        rest = np.stack([cnt, ws], axis=1).reshape(-1).astype(np.uint64)
+        p = m.field.MODULUS
+        return np.array([(int(a) + int(b)) % p for (a, b) in zip(merged.tolist(), rest.tolist())],
+                        dtype="<u8").tobytes()
+
+
+def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None, warmup=None, n_job=None,
+              cpu_baseline=None, emit=True, m=None):
+    """The reference's heavy-hitters driver (examples.py:37-91,
+    mastic_amd.heavy_hitters) over HBM-resident reports: both aggregators'
+    prep_init, the decide and the fold at every level, each level's agg shares
+    merged over RCCL before pruning.  A step = one full level sweep.  Units =
+    sum over levels and aggregators of reports x candidate prefixes.
+
+    Weak scaling (default): every rank sweeps its own `--reports` reports.
+    Strong scaling (split, the north_star job): the job's reports (generated
+    identically on every rank) are divided over the ranks; thresholds use the
+    job total.  --virtual-ranks K (one GPU): rank 0's share of a K-way split,
+    the other ranks' aggregates added in plaintext (VirtualRanksMerge)."""
+    from mastic_amd import Mastic
+    from mastic_amd.heavy_hitters import compute_heavy_hitters
+    from mastic_amd.merge import merge_field_shares
+
+    split = args.split if split is None else split
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    do_cpu = args.cpu_baseline if cpu_baseline is None else cpu_baseline
+    kw = dict(cfg["kw"])
+    bits = kw.pop("bits")
+    if m is None:
+        m = Mastic(bits, cfg["circuit"], device=local, **kw)
+    ctx = b"mastic-mi355x-bench"
+    seed = 0x4D41 + int(cfg.get("seed_digit", args.config[1]))
+    vr = getattr(args, "virtual_ranks", 1) or 1
+    if vr > 1 and (world > 1 or cfg["circuit"] not in ("Count", "Sum")):
+        raise SystemExit("--virtual-ranks: one process, Count or Sum")
+    n_req = n_job or args.reports or cfg["reports"]
+    if split or vr > 1:
+        n_job = n_req
+        (alphas_job, w_job, betas_job, nonces_job, rrng) = sweep_population(cfg, bits, kw, seed, n_job,
+                                                                             seed * 1000003)
+        rands_job = rrng.integers(0, 256, size=m.RAND_SIZE * n_job, dtype=np.uint8)
+        (lo, hi) = split_bounds(n_job, max(world, vr))[rank]
+        n_rep = hi - lo
+        alphas, w = alphas_job[lo:hi], w_job[lo:hi]
+        betas = betas_job[lo:hi].tobytes()
+        nonces = nonces_job[16 * lo:16 * hi].tobytes()
+        rands = rands_job[m.RAND_SIZE * lo:m.RAND_SIZE * hi].tobytes()
+        del betas_job, nonces_job, rands_job
+    else:
+        n_rep = n_req
+        n_job = n_rep * world
+        (alphas, w, betas, nonces, rrng) = sweep_population(cfg, bits, kw, seed, n_rep, seed * 1000003 + rank)
+        betas = betas.tobytes()
+        nonces = nonces.tobytes()
+        rands = rrng.integers(0, 256, size=m.RAND_SIZE * n_rep, dtype=np.uint8).tobytes()
+        alphas_job, w_job = (alphas, w) if world == 1 else (None, None)
+    threshold = sweep_threshold(cfg, kw, n_job)
+    t_sh = time.perf_counter()
+    reps = m.reports_shard(ctx, alphas.tobytes(), betas, nonces, rands)
+    m.synchronize()
+    shard_s = time.perf_counter() - t_sh
     del betas, nonces, rands
     vk = np.random.default_rng(0x4D41).integers(0, 256, size=16, dtype=np.uint8).tobytes()  # gen_rand(16)
     thresholds = {"default": threshold}
-    merge = merge_field_shares(m, dist) if dist else None
+    if vr > 1:
+        merge = VirtualRanksMerge(m, alphas_job[n_rep:], w_job[n_rep:])
+    else:
+        merge = merge_field_shares(m, dist) if dist else None
     if cfg.get("memory_budget_gb"):
         import ctypes
         from mastic_amd import _lib
@@ -242,7 +367,7 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
                                      timing=timing, frontier_cache=bool(args.frontier_cache),
                                      cached_levels=cached_levels)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step(None, None)
     m.synchronize()
     if dist:
@@ -251,7 +376,7 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
     t0 = time.perf_counter()
     traces, timing = [], []
     hh = None
-    for _ in range(args.steps):
+    for _ in range(steps):
         tr = []
         hh = step(tr, timing)
         traces.append(tr)
@@ -260,39 +385,31 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    dt_local = dt
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    units = sum(2 * n_rep * len(lv.prefixes) for tr in traces for lv in tr) * world
-    # plaintext check (single rank): the heavy hitters are exactly the
-    # attributes whose total weight reaches the threshold (every prefix of one
-    # has at least its weight), and sampled levels' aggregates equal the
-    # plaintext prefix sums (talks/func.py:49-80)
+    # units: reports x candidates of both aggregators at every level, over the job
+    # (the ranks' shares sum to the job; a virtual rank reports its own share)
+    n_units = n_rep if vr > 1 else (n_job if split else n_rep * world)
+    units = sum(2 * n_units * len(lv.prefixes) for tr in traces for lv in tr)
+    # plaintext check: the heavy hitters are exactly the attributes whose total
+    # weight reaches the threshold (every prefix of one has at least its
+    # weight), and sampled levels' aggregates equal the plaintext prefix sums
+    # (talks/func.py:49-80); with the job's reports on this rank
     plain_ok = None
-    if world == 1:
-        ab = (bits + 7) // 8
-        arr = np.frombuffer(alpha_b, np.uint8).reshape(-1, ab)
-        keys, inv = np.unique(arr, axis=0, return_inverse=True)
-        tot = np.bincount(inv.ravel(), weights=w)
+    if alphas_job is not None:
+        keys, inv = np.unique(alphas_job, axis=0, return_inverse=True)
+        tot = np.bincount(inv.ravel(), weights=w_job)
         want = set(bytes(k) for (k, t) in zip(keys, tot) if t >= threshold)
         got = set(np.packbits(np.array(p, dtype=bool)).tobytes() for p in hh)
         plain_ok = got == want
         for lv in traces[0][::max(1, len(traces[0]) // 6)]:
-            if not lv.prefixes or lv.level >= 63:
-                continue
-            L = lv.level + 1
-            val = np.zeros(len(arr), dtype=np.uint64)
-            for j in range((L + 7) // 8):
-                val = (val << np.uint64(8)) | arr[:, j].astype(np.uint64)
-            val >>= np.uint64(8 * ((L + 7) // 8) - L)
-            sums = {}
-            u, iv = np.unique(val, return_inverse=True)
-            for (k, t) in zip(u.tolist(), np.bincount(iv.ravel(), weights=w).tolist()):
-                sums[k] = int(t)
-            pv = [int("".join("1" if b else "0" for b in p), 2) for p in lv.prefixes]
-            plain_ok = plain_ok and [sums.get(x, 0) for x in pv] == list(lv.agg_result)
+            if lv.prefixes and lv.level < 64:
+                (_cnt, ws) = prefix_sums(alphas_job, w_job, lv.level, lv.prefixes)
+                plain_ok = plain_ok and ws.tolist() == list(lv.agg_result)
     # node evaluations actually performed: a level served from the frontier cache evaluates
     # only its new tree level (both children of every distinct length-L prefix)
     hit = set(cached_levels)
@@ -304,29 +421,38 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             nodes += 2 * len(set(p[:lv.level] for p in lv.prefixes))
         else:
             nodes += m.tree_stats((lv.level, tuple(lv.prefixes), lv.level == 0))[0]
-    nodes *= 2 * n_rep * args.steps  # both aggregators
+    nodes *= 2 * n_rep * steps  # both aggregators, this rank
     aes_per_node = 1 + (16 + m.VALUE_LEN * m.field.ENCODED_SIZE + 15) // 16
     dom_ops = aes_per_node * AES_BLOCK_OPS + 2 * m.VALUE_LEN * FIELD_ADD_OPS + KECCAK_OPS
     dom_ms = sum(t[0] + t[2] for t in timing)
     n_launch = sum(t[1] for t in timing)
     achieved = nodes * dom_ops / (dom_ms / 1e3) / 1e12 if dom_ms > 0 else 0.0
     widths = [len(lv.prefixes) for lv in traces[0]]
+    if split:
+        scaling, workload = "strong", "%s; the job's %d reports split %d-way (%d on this rank)" % (
+            cfg["desc"], n_job, world, n_rep)
+    elif vr > 1:
+        scaling, workload = "strong", "%s; rank 0 of a virtual %d-way split of %d reports (%d reports), the other "             "ranks' aggregates added in plaintext" % (cfg["desc"], vr, n_job, n_rep)
+    else:
+        scaling, workload = "weak", "%s, %d reports per rank" % (cfg["desc"], n_rep)
     out = {
         "metric": METRIC,
         "value": units / dt,
         "unit": "report*prefix/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / args.steps,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": dt * 1e3 / steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
         "config": {
-            "workload": "%s, %d reports per rank" % (cfg["desc"], n_rep),
-            "reports_per_step": n_rep * world,
+            "workload": workload,
+            "reports_per_step": n_units,
+            "reports_this_rank": n_rep,
+            "job_reports": n_job,
             "threshold": thresholds["default"],
             "levels": len(traces[0]),
             "max_candidates_per_level": max(widths),
@@ -335,9 +461,10 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "heavy_hitters_equal_plaintext": plain_ok,
             "frontier_cache": bool(args.frontier_cache),
             "levels_evaluated_from_cache": len(cached_levels),
-            "node_evals_per_step": nodes // args.steps,
-            "field": "Field64",
-            "parallelism": "reports sharded %d-way, per-level agg-share all-gather + GPU fold" % world,
+            "node_evals_per_step": nodes // steps,
+            "field": "Field64" if m.field.ENCODED_SIZE == 8 else "Field128",
+            "shard_s": shard_s,
+            "parallelism": "reports split %d-way, per-level agg-share all-gather + GPU fold" % world,
         },
         "roofline": {
             "kernel": "k_eval_aes<F64> (+ node-proof waves, + k_node_proof for the last level)",
@@ -354,9 +481,10 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "ops_per_node": dom_ops,
         },
         "breakdown_ms_per_step": {
-            "eval_aes_plus_proofs": dom_ms / args.steps,
-            "absorb": sum(t[4] for t in timing) / args.steps,
-            "prep_init_total": sum(t[6] for t in timing) / args.steps,
+            "eval_aes_plus_proofs": dom_ms / steps,
+            "absorb": sum(t[4] for t in timing) / steps,
+            "prep_init_total": sum(t[6] for t in timing) / steps,
+            "wall_this_rank": dt_local * 1e3 / steps,
         },
     }
     out["rates"] = {
@@ -397,7 +525,8 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
         out["rates"]["spec_literal_sample"] = "%d reports per rank, %d of the sweep's levels (every %d-th), its " \
             "candidate lists, frontier cache off: each level evaluates its whole tree" % (
                 ns, len(lvls), cfg.get("spec_every", 1))
-    if rank == 0 and world == 1 and args.cpu_baseline:
+        del sample
+    if rank == 0 and world == 1 and do_cpu:
         # oracle prep_init (leader) of one report per process at 8 levels spread over the sweep,
         # with the GPU trace's candidate prefixes: a bounded sample of the same workload
         procs = cpu_pool_size(args.cpu_procs)
@@ -418,14 +547,18 @@ def run_sweep(args, cfg, n_rep, world, rank, local, dist, torch):
             "unit": "report*prefix/s",
             "cores": procs,
             "kind": "port",
+            "single_process_value": cu / sum(r[0] for r in res),
             "sample": "%d reports (one per process, spawn pool of %d) x leader prep_init at levels %s of the "
                       "sweep with the GPU run's candidate prefixes; poc-faithful Python oracle with C "
                       "AES/TurboSHAKE" % (procs, procs, [lv.level for lv in lvls]),
         }
-    if rank == 0:
+        out["cpu_baseline"].update(cpu_host_info())
+    del reps
+    if rank == 0 and emit:
         print(json.dumps(out))
-    if dist:
+    if dist and emit:
         dist.destroy_process_group()
+    return out
 
 
 # ---------------------------------------------------------------- launch
@@ -513,9 +646,17 @@ def main():
     cfg = CONFIGS[args.config]
     n_rep = args.reports or cfg["reports"]
     if cfg.get("sweep"):
-        return run_sweep(args, cfg, n_rep, world, rank, local, dist, torch)
+        run_sweep(args, cfg, world, rank, local, dist, torch)
+        return 0
     n_pre = args.prefixes or cfg["prefixes"]
     n_total = max(args.total_reports or cfg.get("total", n_rep), n_rep)
+    n_job = n_total * world
+    if args.split:
+        # --split: the resident reports are the JOB's, divided over the ranks
+        # (the full_job leg is then strong scaling)
+        n_job = n_total
+        (lo, hi) = split_bounds(n_job, world)[rank]
+        n_total = max(n_rep, hi - lo)
     kw = dict(cfg["kw"])
     bits = kw.pop("bits")
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
@@ -685,9 +826,11 @@ def main():
             wall = float(tt.item())
         out["full_job"] = {
             "reports_per_rank": n_total,
+            "job_reports": n_job,
+            "scaling": "strong" if args.split else "weak",
             "prefixes": len(attrs),
             "wall_s": wall,
-            "value": n_total * len(attrs) * world / wall,
+            "value": n_job * len(attrs) / wall,
             "unit": "report*prefix/s",
             "slices": len(bounds),
             "what": "prep_init (leader) + fold of every resident report, %d slices of <= %d, slice agg shares "
@@ -725,6 +868,47 @@ def main():
         }
         out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
+    if args.config == "c2" and args.north_star:
+        # the north_star job (BASELINE.json): bit-exact prep_init + aggregate for
+        # 1M reports x a full 32-bit prefix-level sweep, i.e. the reference's
+        # heavy-hitters driver (examples.py:37-91) over the c2sweep population,
+        # the job's 1M reports split over the ranks (strong scaling).  The C2
+        # context (its ~120 GB work arena) is released first.
+        import gc
+        slices = reps_all = tail = v = None  # noqa: F841
+        m = None
+        gc.collect()
+        ns_cfg = CONFIGS["c2sweep"]
+        ns = run_sweep(args, ns_cfg, world, rank, local, dist, torch, split=True, steps=1, warmup=1,
+                       n_job=ns_cfg["reports"], emit=False)
+        nc = ns["config"]
+        out["north_star"] = {
+            "workload": nc["workload"],
+            "job_reports": nc["job_reports"],
+            "n_gpus": world,
+            "scaling": "strong",
+            "wall_s": ns["ms_per_step"] / 1e3,
+            "value": ns["value"],
+            "unit": ns["unit"],
+            "rate_kind": "frontier cache on (both aggregators' prep_init + decide + fold per level)",
+            "spec_literal_sampled": ns["rates"].get("spec_literal_sampled"),
+            "spec_literal_sample": ns["rates"].get("spec_literal_sample"),
+            "levels": nc["levels"],
+            "levels_evaluated_from_cache": nc["levels_evaluated_from_cache"],
+            "sum_candidates_over_levels": nc["sum_candidates_over_levels"],
+            "threshold": nc["threshold"],
+            "heavy_hitters": nc["heavy_hitters"],
+            "heavy_hitters_equal_plaintext": nc["heavy_hitters_equal_plaintext"],
+            "frac": ns["roofline"]["frac"],
+            "roofline_kernel": ns["roofline"]["kernel"],
+            "breakdown_ms": ns["breakdown_ms_per_step"],
+        }
+        if "cpu_baseline" in ns:
+            cb = ns["cpu_baseline"]
+            out["north_star"]["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind",
+                                                                    "single_process_value", "sample")}
+            out["north_star"]["speedup_vs_cpu_pool"] = ns["value"] / cb["value"]
+            out["north_star"]["speedup_vs_cpu_core"] = ns["value"] / cb["single_process_value"]
     if rank == 0:
         print(json.dumps(out))
     if dist:

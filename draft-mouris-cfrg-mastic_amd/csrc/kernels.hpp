@@ -549,13 +549,7 @@ struct AesArgs {
     const PrefixState* np;          // node-proof prefix state
     int np_f;                       // its fill position
     int aes_waves;                  // waves [0, aes_waves) walk parents, the rest are proof waves
-    int par_waves;                  // items per workgroup = par_waves * ppw (aes_waves, or all 16 waves)
-    // Work items: each parent's payload elements in n_split chunks of
-    // split_len (Field128 circuits with large VALUE_LEN and an identity-like
-    // truncation, tgroup == 1: a C5 parent is 2 x 1,028 AES blocks); an item
-    // recomputes its parent's 4 extend / convert-seed blocks.  1 = whole parents.
-    int n_split;
-    int split_len;
+    int par_waves;                  // parents per workgroup = par_waves * ppw (aes_waves, or all 16 waves)
     int proof_prio;                 // s_setprio of the proof waves
     int aes_prio;                   // s_setprio of the AES waves
     int dbg_skip;                   // timing experiments only (results wrong): 1 = no proof work, 2 = no AES work
@@ -741,8 +735,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     // Parents of this workgroup: [wp0, wp1), claimed in runs of `run` by
     // every wave through an LDS counter: the proof waves join once their
     // proofs are done, so no wave idles while another still has parents.
-    const int wp0 = blockIdx.y * a.par_waves * a.ppw;                  // items
-    const int wp1 = min(wp0 + a.par_waves * a.ppw, a.n_parents * a.n_split);
+    const int wp0 = blockIdx.y * a.par_waves * a.ppw;
+    const int wp1 = min(wp0 + a.par_waves * a.ppw, a.n_parents);
     if (a.dbg_skip & 2) goto aes_done;
     {
     if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -778,7 +772,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             for (int i = 0; i < 4; i++) ps[i] = pld(pl.key + (size_t)i * S, lb);
             pctrl = a.agg_id;
         } else {
-            const int pn = a.parent_node[pi / a.n_split];  // pi: a work item here
+            const int pn = a.parent_node[pi];
 #pragma unroll
             for (int i = 0; i < 4; i++) ps[i] = pld(a.cs_in + ((size_t)pn * 5 + i) * S_in, lb);
             pctrl = pld(a.cs_in + ((size_t)pn * 5 + 4) * S_in, lb);
@@ -787,10 +781,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     uint32_t nps[4], npctrl;
     load_parent(rbeg, nps, npctrl);
     for (int item = rbeg; item >= 0;) {
-        const int pi = item / a.n_split;        // parent
-        const int ch = item - pi * a.n_split;  // element chunk of it
-        const int e_lo = ch * a.split_len;
-        const int e_hi = min(p.value_len, e_lo + a.split_len);
+        const int pi = item;  // parent
+        const int e_lo = 0, e_hi = vl;
         // The key schedules are re-read from LDS (one ds_read_b128 per round):
         // without the barrier the compiler hoists all 22 reads out of the loop
         // and pins 88 VGPRs.
@@ -873,7 +865,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
 #endif
         if constexpr (FC) {
-            if (a.last_cv && ch == 0) {
+            if (a.last_cv) {
                 // convert seeds of the last level's children, staged for the frontier cache
                 const size_t n0 = (size_t)(2 * pi) * 4, n1 = n0 + 4;
 #pragma unroll
@@ -883,7 +875,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 }
             }
         }
-        if (ch == 0) {
+        {
             const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -963,7 +955,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             // stream below redoes this parent from that element on (elements
             // before it are unaffected by the rejection).
             constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
-            const int nblk = (e_hi + EPB - 1) / EPB;  // (e_lo is a multiple of EPB)
+            const int nblk = (e_hi + EPB - 1) / EPB;
             for (int b = e_lo / EPB; b < nblk; b++) {
                 asm volatile("" ::: "memory");
                 const int e = EPB * b;
@@ -1567,24 +1559,27 @@ __global__ __launch_bounds__(256) void k_decide(McParams p, int n, int stride, i
 // of the output is the concatenation of up to 3 plane segments (seg[k]:
 // words[k] planes of stride S), i.e. the prep share eval_proof || [jr_part]
 // || [verifier] (encode_vec is little-endian words, the planes' byte order),
-// or an out share (encode_vec of the truncated vector).  One thread per
-// output word, consecutive threads on consecutive words of a row.
+// or an out share (encode_vec of the truncated vector).  Consecutive threads
+// on consecutive words of a row; a grid-stride loop over the output words (a
+// grid's work-items must stay below 2^32, an output may be larger: C2's
+// 12,288 x 10k-prefix out shares are 2.5e9 words).
 struct RowSegs {
     const uint32_t* seg[3];
     int words[3];
 };
 __global__ __launch_bounds__(256) void k_gather_rows(RowSegs sg, int n, int stride, uint32_t* out) {
-    const int row_words = sg.words[0] + sg.words[1] + sg.words[2];
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (size_t)n * row_words) return;
-    const int r = (int)(i / row_words);
-    int k = (int)(i - (size_t)r * row_words);
-    int s = 0;
-    while (k >= sg.words[s]) {
-        k -= sg.words[s];
-        s++;
+    const size_t row_words = (size_t)sg.words[0] + sg.words[1] + sg.words[2];
+    const size_t total = (size_t)n * row_words;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const int r = (int)(i / row_words);
+        int k = (int)(i - (size_t)r * row_words);
+        int s = 0;
+        while (k >= sg.words[s]) {
+            k -= sg.words[s];
+            s++;
+        }
+        out[i] = sg.seg[s][(size_t)k * stride + r];
     }
-    out[i] = sg.seg[s][(size_t)k * stride + r];
 }
 
 // Both aggregators' prep_shares_to_prep + prep_next outcome per report, from

@@ -123,7 +123,7 @@ inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 // the call (mastic_ctx::graveyard).
 struct LevelCache {
     bool valid = false;
-    uint64_t rep_gen = 0;
+    uint64_t rep_id = 0, rep_gen = 0;  // the batch (mastic_reports::id) and its contents generation
     size_t n = 0;
     size_t S = 0;                               // plane stride (n rounded up to 64, plus padding)
     std::vector<uint8_t> key;                   // u8(len) || verify key || ctx
@@ -147,15 +147,21 @@ struct LevelCache {
 
 }  // namespace
 
-// contents generation (frontier-cache key); contexts may be driven from
-// several threads, so it is atomic
+// Frontier-cache key of a batch: its identity (id, unique per batch or view
+// object) and the generation of the HBM it reads.  A batch and its views share
+// one generation counter (`gen`), so an upload or shard through any of them
+// invalidates cache entries keyed on the others.  Contexts may be driven from
+// several threads, so the counters are atomic.
 static std::atomic<uint64_t> g_reports_gen{0};
 static uint64_t next_reports_gen() { return g_reports_gen.fetch_add(1) + 1; }
 struct mastic_reports {
     mastic_ctx* ctx = nullptr;
     size_t n = 0;
-    uint64_t gen = next_reports_gen();
+    uint64_t id = next_reports_gen();
+    std::shared_ptr<std::atomic<uint64_t>> gen = std::make_shared<std::atomic<uint64_t>>(next_reports_gen());
     DevBuf nonces, pub, in0, in1;
+    void touch() { gen->store(next_reports_gen()); }
+    uint64_t generation() const { return gen->load(); }
 };
 
 struct mastic_ctx {
@@ -199,10 +205,6 @@ struct mastic_ctx {
     size_t chunk_max = 0;        // reports per chunk cap (0 = what fits; MASTIC_CHUNK_REPORTS)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
     int par_waves = 0;           // waves' worth of parents per level-kernel workgroup (0 = by field; MASTIC_PAR_WAVES)
-    // Field128 payload elements per level-kernel work item (MASTIC_SPLIT_ELEMS;
-    // 0 = whole parents, the default: splitting C5's parents into 9 items
-    // measured 3-6 % slower, its step being bound by the binder sponges)
-    int split_elems = 0;
     int pfx_f[PFX_COUNT] = {0};  // fill position of each prefix state (host copy)
     std::vector<uint8_t> pfx_key;  // verify key || ctx of the prefix states in pfx (empty: none)
     std::map<std::vector<uint8_t>, Tree*> trees;
@@ -531,8 +533,17 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         return fail(c, MASTIC_EHIP, "tree upload failed");
     }
     if (c->trees.size() > 64) {
-        (void)hipDeviceSynchronize();  // cached trees may still be read by queued kernels
-        for (auto& kv : c->trees) delete kv.second;
+        // queued kernels may still read the cached trees: their device
+        // buffers are retired (freed at the next idle point of the ctx's
+        // streams, mastic_ctx::bury), not freed here
+        for (auto& kv : c->trees) {
+            for (DevBuf* b : {&kv.second->d_exp, &kv.second->d_pfx, &kv.second->d_path, &kv.second->d_parent}) {
+                if (b->p && b->own) c->graveyard.push_back(b->p);
+                b->p = nullptr;
+                b->bytes = 0;
+            }
+            delete kv.second;
+        }
         c->trees.clear();
     }
     c->trees[keyv] = t;
@@ -812,8 +823,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // the last level's node proofs in the level kernel (after each workgroup's
     // parents) instead of a k_node_proof launch: cache hits, and with
     // MASTIC_FUSE_PROOFS=2 cache-on misses too (whole parents only)
-    const bool fuse_last = (hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs >= 2)) &&
-                           !(p.field == 128 && p.tgroup == 1 && c->split_elems > 0 && p.value_len > c->split_elems);
+    const bool fuse_last = hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs >= 2);
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
         if (!hit && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
@@ -826,15 +836,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // all waves parents from the start: measured neutral on C4 and C2 and
         // 3 % slower on C5 (profiles/r02_v12_ab_level_kernel.json)
         const int par_waves = c->par_waves > 0 ? c->par_waves : EVAL_WAVES - c->proof_waves;
-        // large Field128 payloads: work items of up to split_elems elements
-        // (kernels.hpp AesArgs::n_split; needs tgroup == 1)
-        a.n_split = 1;
-        a.split_len = p.value_len;
-        if (p.field == 128 && p.tgroup == 1 && c->split_elems > 0 && p.value_len > c->split_elems) {
-            a.n_split = (p.value_len + c->split_elems - 1) / c->split_elems;
-            a.split_len = (p.value_len + a.n_split - 1) / a.n_split;
-        }
-        const int n_items = np_ * a.n_split;
+        const int n_items = np_;
         a.ppw = choose_eval_ppw(n_items, groups, par_waves, c->n_cus);
         a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
@@ -1059,7 +1061,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         lc = &c->lc[agg_id];
         const size_t S1 = round_up(n, 64) + pad;
         const int L = t->L;
-        hit = lc->valid && lc->rep_gen == rep->gen && lc->n == n && lc->S == S1 && lc->key == lkey &&
+        hit = lc->valid && lc->rep_id == rep->id && lc->rep_gen == rep->generation() && lc->n == n && lc->S == S1 && lc->key == lkey &&
               !t->weight_check && L == lc->L + 1 && (size_t)L <= lc->n_parents.size() &&
               std::equal(t->n_parents.begin(), t->n_parents.begin() + L, lc->n_parents.begin()) &&
               // level L-1's node paths fix every level above (each level's
@@ -1169,8 +1171,14 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         if (chunk < 64) return fail(c, MASTIC_ENOMEM, "work buffers of 64 reports exceed the memory budget");
         const size_t want = per_report * (chunk + pad);
         const size_t arena = std::max(want, std::min<size_t>(lc ? c->work_arena_fc : c->work_arena, budget));
-        if (!c->work.ensure(arena) && !c->work.ensure(want))
-            return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", want);
+        if (!c->work.ensure(arena) && !c->work.ensure(want)) {
+            // retired buffers (cache slots, evicted trees) are freed once the stream is idle
+            if (c->graveyard.empty() || hipStreamSynchronize(c->stream) != hipSuccess)
+                return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", want);
+            c->bury();
+            if (!c->work.ensure(arena) && !c->work.ensure(want))
+                return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", want);
+        }
         chunk = std::min<size_t>(round_up(n, 64), (c->work.bytes / per_report - pad) / 64 * 64);
     }
     if (c->budget) chunk = std::min(chunk, std::max<size_t>(by_budget, 64));  // an explicit budget caps chunks
@@ -1225,7 +1233,8 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     for (void* q : retire_after) c->graveyard.push_back(q);
     if (lc) {
         lc->valid = true;
-        lc->rep_gen = rep->gen;
+        lc->rep_id = rep->id;
+        lc->rep_gen = rep->generation();
         lc->n = n;
         lc->key = lkey;
         lc->L = t->L;
@@ -1245,8 +1254,10 @@ static int gather_rows(mastic_ctx* c, const RowSegs& sg, size_t n, size_t stride
     const size_t words = (size_t)sg.words[0] + sg.words[1] + sg.words[2];
     if (n == 0 || words == 0) return 0;
     const size_t total = n * words;
-    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream, sg, (int)n,
-                       (int)stride, (uint32_t*)dst);
+    // grid-stride kernel: at most 2^20 workgroups (2^28 work-items) per launch
+    const size_t blocks = std::min<size_t>((total + 255) / 256, (size_t)1 << 20);
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(256), 0, c->stream, sg, (int)n, (int)stride,
+                       (uint32_t*)dst);
     HIPCHK(c, hipGetLastError());
     return 0;
 }
@@ -1388,13 +1399,20 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     return 0;
 }
 
-extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share) {
+extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share,
+                                       void* caller_stream) {
     DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     Result& R = c->res[agg_id];
     if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
     const size_t rows = (size_t)R.n_prefixes * (1 + c->p.output_len);
     if (rows && !dev_agg_share) return fail(c, MASTIC_EINVAL, "null agg share buffer");
+    // the buffer may have been allocated / filled by work queued on the
+    // caller's stream (e.g. a torch allocation's fill): the fold writes it
+    // only after that work, ordered by an event (no device-wide sync)
+    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->fold_ev, (hipStream_t)caller_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->fold_ev, 0));
     int rc = aggregate_impl(c, agg_id, valid, (uint32_t*)dev_agg_share);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's stream (e.g. RCCL's) reads it next
@@ -1610,6 +1628,7 @@ extern "C" int mastic_reports_view(mastic_reports* rep, size_t first, size_t cou
     mastic_reports* r = new mastic_reports();
     r->ctx = c;
     r->n = count;
+    r->gen = rep->gen;  // one contents generation for the batch and all its views
     const size_t ps = mc_public_share_size(p), i0 = mc_input_share_size(p, 0), i1 = mc_input_share_size(p, 1);
     r->nonces.view(rep->nonces, 16 * first, 16 * count);
     r->pub.view(rep->pub, ps * first, ps * count);
@@ -1632,7 +1651,7 @@ extern "C" int mastic_reports_upload(mastic_reports* r, const uint8_t* nonces, c
     mastic_ctx* c = r->ctx;
     const McParams& p = c->p;
     const size_t n = r->n;
-    r->gen = next_reports_gen();
+    r->touch();
     if (nonces) HIPCHK(c, hipMemcpy(r->nonces.p, nonces, 16 * n, hipMemcpyHostToDevice));
     if (pub) HIPCHK(c, hipMemcpy(r->pub.p, pub, (size_t)mc_public_share_size(p) * n, hipMemcpyHostToDevice));
     if (in0) {
@@ -1747,7 +1766,7 @@ extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx,
     DeviceScope ds_(rep ? rep->ctx : nullptr);
     if (!rep) return MASTIC_EINVAL;
     mastic_ctx* c = rep->ctx;
-    rep->gen = next_reports_gen();
+    rep->touch();
     if (rep->n == 0) return 0;
     if (!alphas || !nonces || !rands || (!betas && c->p.meas_len > 0)) return fail(c, MASTIC_EINVAL, "null input");
     int rc = build_prefixes(c, app_ctx, ctx_len, nullptr, 0);
@@ -1790,6 +1809,18 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->p = p;
     c->device = up->device;
     c->n_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // Test hook (MASTIC_FORCE_SLOW_BLK, result-preserving): the payload fast
+    // path hands over to the exact rejection-sampling stream at this block, so
+    // the tests reach the handover that random data hits with probability
+    // 2^-32 per candidate.  Outputs are identical either way.
+    {
+        const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
+        c->force_slow_blk = fs ? atoi(fs) : -1;
+    }
+#ifdef MASTIC_EXPERIMENT_KNOBS
+    // A/B and timing experiments only (tools/ab_*.sh build the library with
+    // -DMASTIC_EXPERIMENT_KNOBS; the shipped library reads none of these).
+    // MASTIC_DBG_SKIP and MASTIC_ABSORB_DBG skip or gut kernels: results wrong.
     {
         const char* e = getenv("MASTIC_ABSORB_SINGLE");
         c->absorb_pair = !(e && e[0] == '1');
@@ -1815,8 +1846,6 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (xp) c->aes_prio = std::max(0, std::min(2, atoi(xp)));
         const char* pp = getenv("MASTIC_PROOF_PRIO");
         if (pp) c->proof_prio = std::max(0, std::min(2, atoi(pp)));
-        const char* se = getenv("MASTIC_SPLIT_ELEMS");
-        if (se) c->split_elems = std::max(0, atoi(se));
         const char* pw2 = getenv("MASTIC_PAR_WAVES");
         if (pw2) c->par_waves = std::max(1, std::min(EVAL_WAVES, atoi(pw2)));
         const char* cp = getenv("MASTIC_CHUNK_PIPELINE");
@@ -1827,9 +1856,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (fa) c->fc_all = fa[0] == '1';
         const char* cr = getenv("MASTIC_CHUNK_REPORTS");
         if (cr) c->chunk_max = (size_t)std::max(0, atoi(cr));
-        const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
-        c->force_slow_blk = fs ? atoi(fs) : -1;
     }
+#endif
     // the level kernel's LDS (table + key schedules) is dynamic, above the
     // 64 KiB default
     if (hipFuncSetAttribute((const void*)k_eval_aes<F64, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1876,14 +1904,16 @@ extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
     if (on >= 0) {
         c->frontier_cache = on != 0;
         if (!on) {
-            // queued kernels may still read the cache buffers
-            (void)hipStreamSynchronize(c->stream);
-            (void)hipStreamSynchronize(c->stream2);
-            (void)hipStreamSynchronize(c->stream3);
-        }
-        if (!on) {
-            for (auto& x : c->lc) x.release();
-            c->bury();
+            // queued kernels may still read the cache slots: retire them (freed
+            // at the next idle point of the ctx's streams), no synchronisation
+            for (auto& x : c->lc) {
+                for (DevBuf* b : {&x.sp, &x.rootsum, &x.cs, &x.cv}) {
+                    if (b->p && b->own) c->graveyard.push_back(b->p);
+                    b->p = nullptr;
+                    b->bytes = 0;
+                }
+                x.release();
+            }
         }
     }
     if (last_hit) *last_hit = c->last_hit ? 1 : 0;

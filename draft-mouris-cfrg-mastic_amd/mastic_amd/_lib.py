@@ -62,21 +62,26 @@ class MasticError(RuntimeError):
         self.code = code
 
 
-def build(verbose=False, force=False) -> str:
-    """Compile csrc/mastic_hip.hip for gfx950 into the package directory."""
+def build(verbose=False, force=False, out=None, defines=()) -> str:
+    """Compile csrc/mastic_hip.hip for gfx950 into the package directory.
+    ``out`` / ``defines``: another build of the same source (e.g.
+    ``defines=("MASTIC_EXPERIMENT_KNOBS",)`` for the A/B tools, loaded through
+    MASTIC_LIB); the shipped library is the default one."""
+    out = out or LIB_PATH
     srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
     srcs.append(os.path.join(INCLUDE, "mastic_hip.h"))
     newest = max(os.path.getmtime(s) for s in srcs)
-    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
-        return LIB_PATH
-    tmp = LIB_PATH + ".%d.tmp" % os.getpid()
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+        return out
+    tmp = out + ".%d.tmp" % os.getpid()
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I" + INCLUDE, "-o", tmp, os.path.join(CSRC, "mastic_hip.hip")]
+           "-I" + INCLUDE] + ["-D" + d for d in defines] + ["-o", tmp, os.path.join(CSRC, "mastic_hip.hip")]
     if verbose:
         print(" ".join(cmd))
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, out)
+    return out
 
 
 _lib = None
@@ -119,7 +124,7 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
                     "mastic_fold_shares": (i32, [P, P, sz, sz, P, P]),
-                    "mastic_aggregate_device": (i32, [P, i32, P, P]),
+                    "mastic_aggregate_device": (i32, [P, i32, P, P, P]),
                     "mastic_reports_view": (i32, [P, sz, sz, ctypes.POINTER(P)]),
                     "mastic_decide_results": (i32, [P, u8p, sz, P, P]),
                     "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3

@@ -146,6 +146,8 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
             enc = mastic.encode_agg_param(agg_param)
 
         device_merge = fast and merge is not None and hasattr(merge, "total")
+        if merge is not None and hasattr(merge, "begin_level"):
+            merge.begin_level(level, prefixes)  # merges that need the level's candidates
         n_elems = len(prefixes) * (1 + mastic.OUTPUT_LEN) if device_merge else 0
         raw = agg_shares = None
         if n and prefixes:

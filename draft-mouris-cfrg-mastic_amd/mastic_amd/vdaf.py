@@ -235,11 +235,14 @@ class Mastic:
         """Make last_timing* report agg_id's last prep_init (waits for it)."""
         _check(self._ctx, _lib.lib().mastic_prep_result(self._ctx, agg_id, None, None, None, None))
 
-    def aggregate_to(self, agg_id: int, valid, dev_ptr: int):
+    def aggregate_to(self, agg_id: int, valid, dev_ptr: int, stream: int = 0):
         """``mastic_aggregate_device``: fold into caller-owned device memory
-        (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM."""
+        (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM.
+        ``stream`` is the hipStream_t handle whose queued work last touched
+        the buffer (0 = the null stream)."""
         v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-        _check(self._ctx, _lib.lib().mastic_aggregate_device(self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr)))
+        _check(self._ctx, _lib.lib().mastic_aggregate_device(self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr),
+                                                             ctypes.c_void_p(stream or None)))
 
     def aggregate_device(self, agg_id: int, agg_param, valid=None, raw=False):
         """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU
@@ -578,6 +581,13 @@ class Reports:
         v.n = count
         v._parent = self
         return v
+
+    def upload(self, nonces: bytes, public_shares: bytes, input_shares_0=None, input_shares_1=None):
+        """Overwrite this batch's reports in place (``mastic_reports_upload``);
+        a view and the batch it views share HBM, so either sees the new data."""
+        _check(self._m._ctx, _lib.lib().mastic_reports_upload(
+            self._ptr, _lib.buf(nonces), _lib.buf(public_shares), _lib.buf(input_shares_0),
+            _lib.buf(input_shares_1)))
 
     def download(self):
         m = self._m

@@ -144,8 +144,12 @@ int mastic_decide_results(mastic_ctx* ctx, const uint8_t* app_ctx, size_t ctx_le
 int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t* agg_share);
 /* mastic_aggregate into a caller-owned DEVICE buffer of the ctx's GPU (same
  * layout), e.g. the send buffer of an RCCL all-gather: the share never
- * leaves HBM.  Returns when the buffer is written. */
-int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share);
+ * leaves HBM.  caller_stream is the hipStream_t whose queued work last
+ * touched the buffer (e.g. the stream it was allocated or zero-filled on;
+ * NULL = the null stream): the fold is ordered after that work by an event.
+ * Returns when the buffer is written. */
+int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
+                            void* caller_stream);
 /* Multi-GPU merge (Mastic.merge, mastic.py:390-397) of n_shares agg shares
  * of n_elems elements each, all in DEVICE memory of the ctx's GPU (e.g. the
  * output of an RCCL all-gather): dev_out[e] = sum_s dev_shares[s][e] mod p.

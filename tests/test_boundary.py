@@ -60,3 +60,27 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
                 text = open(os.path.join(dirpath, f), errors="replace").read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", text).replace("CPU oracle", ""), f
+
+
+def test_shipped_library_reads_no_experiment_knobs():
+    """The A/B timing knobs (some skip or gut kernels, e.g. MASTIC_DBG_SKIP,
+    MASTIC_ABSORB_DBG) are compiled only into -DMASTIC_EXPERIMENT_KNOBS
+    builds: the shipped library does not even contain their names, so a stray
+    variable in an aggregator's environment cannot change its results.  The
+    only variable it reads that touches computation is the result-preserving
+    test hook MASTIC_FORCE_SLOW_BLK (exact-stream handover)."""
+    data = open(_lib_path(), "rb").read()
+    for knob in (b"MASTIC_DBG_SKIP", b"MASTIC_ABSORB_DBG", b"MASTIC_ABSORB_SINGLE", b"MASTIC_PROOF_WAVES",
+                 b"MASTIC_BINDER_TILED", b"MASTIC_CHUNK_REPORTS", b"MASTIC_SPLIT_ELEMS", b"MASTIC_FC_ALL"):
+        assert knob not in data, knob
+    assert b"MASTIC_FORCE_SLOW_BLK" in data
+
+
+def test_product_has_no_device_wide_sync():
+    """Product-path ordering uses the ctx's own streams and events: no
+    hipDeviceSynchronize anywhere in the library source (a device-wide sync
+    would also wait for RCCL's and torch's streams on that GPU)."""
+    csrc = os.path.join(ROOT, "draft-mouris-cfrg-mastic_amd", "csrc")
+    for f in os.listdir(csrc):
+        text = re.sub(r"//.*", "", open(os.path.join(csrc, f)).read())
+        assert "hipDeviceSynchronize" not in text, f

@@ -229,3 +229,39 @@ def test_cache_at_c3_parameters(mastic_amd):
         m_on.set_frontier_cache(False)
     assert hits >= 2 * 200, hits
     assert len(checked) == 3, checked
+
+
+def test_cache_tracks_writes_through_views(mastic_amd):
+    """A batch and its views share HBM and one contents generation: new
+    reports uploaded through the parent batch invalidate a cache filled
+    through a view (the next level evaluates its whole tree, equal to a
+    cache-off context on the new data), and two views of equal size at
+    different offsets never share cache entries."""
+    rng = random.Random(81)
+    m = mastic_amd.MasticCount(6)
+    ref = mastic_amd.MasticCount(6)
+    (alphas, weights, nonces, rands) = _reports(m, rng, 128, 4)
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    (alphas2, weights2, nonces2, rands2) = _reports(m, rng, 128, 4)
+    (pub2, in0_2, in1_2) = m.shard_batch(CTX, alphas2, weights2, nonces2, rands2)
+    allr = m.reports_upload(nonces, pub, in0, in1)
+    v0 = allr.view(0, 64)
+    v1 = allr.view(64, 64)
+    m.set_frontier_cache(True)
+    vk = bytes(range(16))
+    lvl0 = (0, ((False,), (True,)), False)
+    lvl1 = (1, ((False, False), (False, True), (True, False), (True, True)), False)
+    m.prep_init_device(v0, vk, CTX, 0, lvl0)
+    m.prep_init_device(v0, vk, CTX, 0, lvl1)
+    assert m.last_prep_was_cached()
+    m.prep_init_device(v0, vk, CTX, 0, lvl0)
+    m.prep_init_device(v1, vk, CTX, 0, lvl1)  # same size, other reports
+    assert not m.last_prep_was_cached()
+    m.prep_init_device(v0, vk, CTX, 0, lvl0)
+    allr.upload(nonces2, pub2, in0_2, in1_2)  # new data through the parent
+    m.prep_init_device(v0, vk, CTX, 0, lvl1)
+    assert not m.last_prep_was_cached()
+    got = m.prep_result(v0, 0, lvl1, want_out_shares=True)
+    want = ref.prep_init_batch(vk, CTX, 0, lvl1, nonces2[:16 * 64], pub2[:len(pub2) // 2], in0_2[:len(in0_2) // 2])
+    assert got[0] == want[0] and got[2] == want[2]
+    m.set_frontier_cache(False)

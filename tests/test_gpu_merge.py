@@ -188,3 +188,30 @@ def test_decide_results_on_device_matches_host_decide(torch_cuda):
             want &= joint_rand_confirmed(msgs, sh[0][1], sh[1][1], n)
             assert not want[3]
         assert list(acc == 1) == list(want)
+
+
+def test_aggregate_device_waits_for_callers_stream(torch_cuda):
+    """mastic_aggregate_device writes a buffer that the caller prepared on its
+    own stream: queue a long busy kernel and then a fill of the buffer on
+    torch's current stream, fold into it, and the fold must land after the
+    fill (the library orders itself after that stream by an event)."""
+    torch = torch_cuda
+    import mastic_amd
+    from mastic_amd.merge import aggregate_to_tensor
+    rng = random.Random(8)
+    m = mastic_amd.MasticSum(6, 9)
+    ctx = b"order"
+    (alphas, weights, nonces, rands) = _shard(m, rng, 130, ctx)
+    (pub, in0, in1) = m.shard_batch(ctx, alphas, weights, nonces, rands)
+    reps = m.reports_upload(nonces, pub, in0, in1)
+    cand = tuple(sorted(set(alphas[:30])))
+    enc = m.encode_agg_param((5, cand, True))
+    n_elems = len(cand) * (1 + m.OUTPUT_LEN)
+    m.prep_init_device(reps, bytes(16), ctx, 0, enc)
+    want = m.aggregate_device(0, enc, raw=True)
+    for _ in range(3):
+        out = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device="cuda")
+        torch.cuda._sleep(50_000_000)  # ~20 ms of busy work ahead of the fill on torch's stream
+        out.fill_(0xA5)
+        aggregate_to_tensor(m, 0, n_elems, out=out)
+        assert out.cpu().numpy().tobytes() == want

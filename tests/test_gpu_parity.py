@@ -515,14 +515,12 @@ def test_c2_full_prefix_count_oracle_report(mastic_amd):
 
 
 @pytest.mark.parametrize("blk", [-1, 0, 150, 250])
-def test_field128_element_split_work_items(mastic_amd, blk, monkeypatch):
-    """Large Field128 payloads (VALUE_LEN 301 > 128) are evaluated as work
-    items of ~101 elements each (three per parent, each recomputing its
-    parent's extend / convert-seed blocks).  Every output against the oracle,
-    also with the exact-stream handover forced inside the 1st / 2nd / 3rd
-    chunk (the exact stream restarts from element 0 and emits only its
-    chunk's elements)."""
-    monkeypatch.setenv("MASTIC_SPLIT_ELEMS", "128")  # (off by default)
+def test_field128_long_payload_handover(mastic_amd, blk, monkeypatch):
+    """A long Field128 payload (VALUE_LEN 301: 301 convert blocks per child,
+    the C5 shape at a smaller length).  Every output against the oracle, also
+    with the exact-stream handover forced early, in the middle and near the
+    end of the payload (the exact stream restarts from element 0 and emits
+    from the handover element on)."""
     if blk >= 0:
         monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
     rng = random.Random(400 + blk)

@@ -2,7 +2,7 @@
 are split across ranks, each rank produces its aggregate share, the shares are
 all-gathered in rank order (mastic_amd.merge.gather_shares) and their GF(p)
 sum equals the aggregate of the whole report set.  The field sum here is the
-oracle's (the GPU fold kernel itself is covered by tests/test_gpu_parity.py)."""
+oracle's (the GPU fold kernel itself is covered by tests/test_gpu_merge.py)."""
 import os
 import random
 import socket
