@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "host_tree.hpp"
 #include "kernels.hpp"
 #include "shard.hpp"
 
@@ -81,20 +82,9 @@ struct DevBuf {
     template <class T> T* as() const { return (T*)p; }
 };
 
-struct Tree {
-    int L = 0;
-    int n_prefixes = 0;
-    bool weight_check = false;
-    std::vector<int> n_parents;        // per level
-    std::vector<int> n_exp;            // expanded nodes per level
-    std::vector<size_t> off;           // per-level offset into the node arrays
-    std::vector<int32_t> child_exp, child_pfx;
-    std::vector<uint32_t> child_path;  // 8 words per node
-    std::vector<size_t> poff;          // per-level offset into parent_node
-    std::vector<int32_t> parent_node;  // node index (in level l-1) of every parent of level l
+// The decoded agg param's tree (host_tree.hpp) plus its device copy.
+struct Tree : TreeShape {
     DevBuf d_exp, d_pfx, d_path, d_parent;
-    uint64_t nodes = 0, interior = 0;
-    int max_level_nodes = 0, max_exp = 0, max_parents = 0;
 };
 
 struct Result {
@@ -400,119 +390,14 @@ static int build_tree(mastic_ctx* c, const uint8_t* enc, size_t len, Tree** out)
         *out = it->second;
         return 0;
     }
-    if (len < 7) return fail(c, MASTIC_EINVAL, "agg param too short");
-    const int level = (enc[0] << 8) | enc[1];
-    const uint64_t count = ((uint64_t)enc[2] << 24) | ((uint64_t)enc[3] << 16) | ((uint64_t)enc[4] << 8) | enc[5];
-    const size_t plen = (size_t)(level + 1 + 7) / 8;
-    if (len != 6 + plen * count + 1) return fail(c, MASTIC_EINVAL, "agg param has incorrect length");
-    if (level >= c->p.bits) return fail(c, MASTIC_EINVAL, "level too deep");
-    if (enc[len - 1] > 1) return fail(c, MASTIC_EINVAL, "invalid weight check flag");
-    // the poc cannot evaluate an empty candidate set either (eval_with_siblings leaves the
-    // root's children unset and prep_init fails at mastic.py:270)
-    if (count == 0) return fail(c, MASTIC_EINVAL, "empty candidate prefix list");
-    const uint8_t* pre = enc + 6;
-    // prefixes as MSB-first byte strings of plen bytes (bits past level+1 must be zero)
-    const int tail_bits = (level + 1) % 8;
-    std::vector<std::vector<uint8_t>> pfx(count);
-    for (uint64_t i = 0; i < count; i++) {
-        pfx[i].assign(pre + plen * i, pre + plen * (i + 1));
-        if (tail_bits && (pfx[i][plen - 1] & ((1u << (8 - tail_bits)) - 1)))
-            return fail(c, MASTIC_EINVAL, "prefix with incorrect length");
-    }
-    // Sorted candidate order (lexicographic = MSB-first bit order) and the
-    // common-prefix length in bits of each adjacent pair: the distinct
-    // length-m prefixes are the runs of sorted candidates split wherever the
-    // adjacent common prefix is shorter than m, so every level's expanded
-    // nodes, child indices and paths come from O(count) scans (no per-level
-    // sorting, searching or allocation).
-    std::vector<int> order(count);
-    for (uint64_t i = 0; i < count; i++) order[i] = (int)i;
-    std::sort(order.begin(), order.end(), [&](int a, int b) { return pfx[a] < pfx[b]; });
-    auto bit_of = [&](int s, int l) { return (pfx[order[s]][l / 8] >> (7 - l % 8)) & 1; };
-    std::vector<int> lcp(count, -1);  // lcp[0] = -1: always starts a run
-    for (uint64_t s = 1; s < count; s++) {
-        const std::vector<uint8_t>& a = pfx[order[s - 1]];
-        const std::vector<uint8_t>& b = pfx[order[s]];
-        int bits = 0;
-        size_t k = 0;
-        while (k < plen && a[k] == b[k]) k++;
-        if (k == plen) return fail(c, MASTIC_EINVAL, "candidate prefixes are non-unique");
-        bits = (int)k * 8;
-        if (k < plen) bits += __builtin_clz((unsigned)(a[k] ^ b[k])) - 24;
-        lcp[s] = bits;
-    }
-
     Tree* t = new Tree();
-    t->L = level;
-    t->n_prefixes = (int)count;
-    t->weight_check = enc[len - 1] == 1;
-    size_t total = 0;
-    std::vector<int> run_begin;           // runs of length-l prefixes = parents of level l
-    std::vector<int> gid_next(count, 0);  // run index of each sorted candidate at length l+1
-    run_begin.push_back(0);               // level 0: the root (one run over all candidates)
-    for (int l = 0; l <= level; l++) {
-        const int np = (int)run_begin.size();
-        t->n_parents.push_back(np);
-        t->poff.push_back(t->parent_node.size());
-        if (l > 0) {
-            // parents of level l are level l-1's expanded nodes; find their node index
-            const size_t prev = t->off[l - 1];
-            const int prev_nodes = 2 * t->n_parents[l - 1];
-            for (int k = 0; k < prev_nodes; k++)
-                if (t->child_exp[prev + k] >= 0) t->parent_node.push_back(k);
-        }
-        int n_next = 0;
-        std::vector<int> next_begin;
-        if (l < level) {
-            for (uint64_t s = 0; s < count; s++) {
-                if (lcp[s] < l + 1) {
-                    next_begin.push_back((int)s);
-                    n_next++;
-                }
-                gid_next[s] = n_next - 1;
-            }
-        }
-        t->n_exp.push_back(n_next);
-        t->off.push_back(total);
-        const int nb = (l + 1 + 7) / 8;  // path bytes at this level
-        for (int pi = 0; pi < np; pi++) {
-            const int b = run_begin[pi];
-            const int e = pi + 1 < np ? run_begin[pi + 1] : (int)count;
-            const std::vector<uint8_t>& rep = pfx[order[b]];
-            for (int cbit = 0; cbit < 2; cbit++) {
-                // child cbit exists iff the run's first (cbit 0) / last (cbit 1)
-                // member has that bit at position l
-                const int m = cbit ? e - 1 : b;
-                const bool exists = bit_of(m, l) == cbit;
-                int ce = -1, cp = -1;
-                if (exists) {
-                    if (l < level)
-                        ce = gid_next[m];
-                    else
-                        cp = order[m];
-                }
-                t->child_exp.push_back(ce);
-                t->child_pfx.push_back(cp);
-                // path: the parent's l bits, then cbit (bits past l + 1 zero)
-                uint32_t w[8] = {0};
-                for (int bi = 0; bi < nb; bi++) {
-                    uint32_t byte = rep[bi];
-                    const int lo = bi * 8;
-                    if (lo + 8 > l) byte = lo >= l ? 0u : (byte & ((0xFF00u >> (l - lo)) & 0xFFu));
-                    if (cbit && bi == l / 8) byte |= 0x80u >> (l % 8);
-                    w[bi / 4] |= byte << (8 * (bi % 4));
-                }
-                for (int k = 0; k < 8; k++) t->child_path.push_back(w[k]);
-            }
-        }
-        total += 2 * (size_t)np;
-        t->max_level_nodes = std::max(t->max_level_nodes, 2 * np);
-        t->max_parents = std::max(t->max_parents, np);
-        t->max_exp = std::max(t->max_exp, t->n_exp.back());
-        if (l > 0) t->interior += np;
-        run_begin.swap(next_begin);
+    std::string perr;
+    const int prc = tree_parse(c->p.bits, enc, len, t, &perr);
+    if (prc != TREE_OK) {
+        delete t;
+        return fail(c, prc == TREE_ENOMEM ? MASTIC_ENOMEM : MASTIC_EINVAL, "%s", perr.c_str());
     }
-    t->nodes = total;
+    const size_t total = t->nodes;
     const size_t npar = std::max<size_t>(t->parent_node.size(), 1);
     if (!t->d_exp.ensure(total * 4) || !t->d_pfx.ensure(total * 4) || !t->d_path.ensure(total * 32) ||
         !t->d_parent.ensure(npar * 4)) {
@@ -1797,6 +1682,7 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     if (mc_derive((int)up->circuit, (int)up->bits, (int)up->length, (int)up->sum_vec_bits, up->max_measurement,
                   (int)up->chunk_length, &p))
         return MASTIC_EINVAL;
+    if (p.bits > TREE_MAX_BITS) return MASTIC_EINVAL;  // node paths are at most 256 bits (host_tree.hpp)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MASTIC_ENODEV;
     if (up->device < 0 || up->device >= ndev) return MASTIC_ENODEV;

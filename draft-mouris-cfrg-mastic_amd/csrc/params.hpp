@@ -1,7 +1,13 @@
 // Mastic instantiation parameters (poc/mastic.py:81-89, :567-614) and the
 // FLP shape of each validity circuit (vdaf_poc.flp_bbcggi19, vdaf-13).
 #pragma once
+#ifdef __HIP__
 #include "common.hpp"
+#else
+// host-only build of the parameter logic (tests/host/fuzz_host.cpp, sanitizers)
+#include <stdint.h>
+#define MH_HD inline
+#endif
 
 enum McCircuit : int {
     MC_COUNT = 1,
@@ -60,6 +66,10 @@ MH_HD int mc_bit_length(uint64_t x) {
     return b;
 }
 
+// Largest SumVec / Histogram / MultihotCountVec length and chunk length
+// accepted (the reference has no limit; these keep every size in int range).
+#define MC_MAX_LENGTH (1 << 22)
+
 // Returns 0 on success, -1 on invalid parameters.
 inline int mc_derive(int circuit, int bits, int length, int sv_bits, uint64_t max_measurement,
                      int chunk, McParams* out) {
@@ -88,7 +98,8 @@ inline int mc_derive(int circuit, int bits, int length, int sv_bits, uint64_t ma
         p.tgroup = p.wbits; p.tlimit = p.wbits; p.alg_id = 0xFFFF0002u;
         break;
     case MC_SUMVEC:
-        if (length < 1 || sv_bits < 1 || sv_bits > 63 || chunk < 1) return -1;
+        if (length < 1 || length > MC_MAX_LENGTH || sv_bits < 1 || sv_bits > 63 || chunk < 1 || chunk > MC_MAX_LENGTH)
+            return -1;
         p.field = 128; p.gadget = G_PSUM_MUL; p.arity = 2 * chunk;
         p.calls = (length * sv_bits + chunk - 1) / chunk;
         p.meas_len = length * sv_bits; p.output_len = length; p.eval_output_len = 1;
@@ -96,7 +107,7 @@ inline int mc_derive(int circuit, int bits, int length, int sv_bits, uint64_t ma
         p.tgroup = sv_bits; p.tlimit = length * sv_bits; p.alg_id = 0xFFFF0003u;
         break;
     case MC_HISTOGRAM:
-        if (length < 1 || chunk < 1) return -1;
+        if (length < 1 || length > MC_MAX_LENGTH || chunk < 1 || chunk > MC_MAX_LENGTH) return -1;
         p.field = 128; p.gadget = G_PSUM_MUL; p.arity = 2 * chunk;
         p.calls = (length + chunk - 1) / chunk;
         p.meas_len = length; p.output_len = length; p.eval_output_len = 2;
@@ -104,7 +115,8 @@ inline int mc_derive(int circuit, int bits, int length, int sv_bits, uint64_t ma
         p.tgroup = 1; p.tlimit = length; p.alg_id = 0xFFFF0004u;
         break;
     case MC_MULTIHOT:
-        if (length < 1 || chunk < 1 || max_measurement == 0) return -1;
+        if (length < 1 || length > MC_MAX_LENGTH || chunk < 1 || chunk > MC_MAX_LENGTH || max_measurement == 0)
+            return -1;
         p.field = 128; p.gadget = G_PSUM_MUL; p.arity = 2 * chunk;
         p.wbits = mc_bit_length(max_measurement);
         if (p.wbits > 63) return -1;
@@ -126,6 +138,9 @@ inline int mc_derive(int circuit, int bits, int length, int sv_bits, uint64_t ma
     p.query_rand_len = 1 + (p.eval_output_len > 1 ? p.eval_output_len : 0);
     p.proof_len = p.arity + p.degree * (p.P - 1) + 1;
     p.verifier_len = 1 + p.arity + 1;
+    // every wire size must fit the int arithmetic of the size helpers below
+    const uint64_t pub = (uint64_t)(2 * bits + 7) / 8 + 48ull * (uint64_t)bits + (uint64_t)bits * p.value_len * p.enc;
+    if (pub > (uint64_t)INT32_MAX / 2 || (uint64_t)p.proof_len * p.enc > (uint64_t)INT32_MAX / 4) return -1;
     *out = p;
     return 0;
 }
