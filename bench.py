@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--total-reports", type=int, default=0,
                     help="reports resident in HBM per rank; steps walk distinct --reports slices of them "
                          "(0 = config default: 1M for c2)")
+    ap.add_argument("--pool-reports", type=int, default=0,
+                    help="distinct reports resident per rank (0 = all of --total-reports); a larger job cycles "
+                         "through the pool slice by slice (SURVEY §8d: C5's cycled pool of 2^16 reports)")
     ap.add_argument("--full-job", type=int, default=-1,
                     help="also time prep_init+aggregate over all resident reports (-1 = config default)")
     ap.add_argument("--agg-id", type=int, default=0)
@@ -386,6 +389,8 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         dist.barrier()
     dt = time.perf_counter() - t0
     dt_local = dt
+    (free_b, total_b) = torch.cuda.mem_get_info()
+    hbm_used = (total_b - free_b) / 1e9  # whole device, arena and frontier cache included
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -464,6 +469,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             "node_evals_per_step": nodes // steps,
             "field": "Field64" if m.field.ENCODED_SIZE == 8 else "Field128",
             "shard_s": shard_s,
+            "hbm_used_gb_after": hbm_used,
             "parallelism": "reports split %d-way, per-level agg-share all-gather + GPU fold" % world,
         },
         "roofline": {
@@ -662,7 +668,11 @@ def main():
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
-    attrs, alpha_b, betas, nonces, rands = synth(m, cfg, rank, n_total, n_pre, seed)
+    # distinct reports resident in HBM: all of them, or a pool the job cycles through
+    n_res = n_total
+    if args.pool_reports and args.pool_reports < n_total:
+        n_res = max(n_rep, args.pool_reports // n_rep * n_rep)
+    attrs, alpha_b, betas, nonces, rands = synth(m, cfg, rank, n_res, n_pre, seed)
     vk = np.random.default_rng(0x4D41).integers(0, 256, size=32, dtype=np.uint8).tobytes()
     enc_ap = agg_param_bytes(bits - 1, attrs)
     # the whole job's reports resident in HBM (GPU shard); each step runs the
@@ -672,7 +682,7 @@ def main():
     m.synchronize()
     shard_s = time.perf_counter() - t_sh
     del alpha_b, betas, nonces, rands
-    slices = [reps_all.view(i * n_rep, n_rep) for i in range(n_total // n_rep)]
+    slices = [reps_all.view(i * n_rep, n_rep) for i in range(n_res // n_rep)]
     (nodes, interior, _maxl) = m.tree_stats(enc_ap)
     n_elems = len(attrs) * (1 + m.OUTPUT_LEN)
 
@@ -801,7 +811,7 @@ def main():
         # agg share (out shares of 1M x 10k prefixes = 160 GB cannot be
         # materialised at once, so the job is necessarily sliced)
         bounds = [(i, min(n_rep, n_total - i)) for i in range(0, n_total, n_rep)]
-        tail = reps_all.view(bounds[-1][0], bounds[-1][1]) if bounds[-1][1] != n_rep else None
+        tail = reps_all.view(0, bounds[-1][1]) if bounds[-1][1] != n_rep else None
         m.synchronize()
         if dist:
             dist.barrier()
@@ -809,7 +819,7 @@ def main():
         t1 = time.perf_counter()
         parts = []
         for (j, (first, cnt)) in enumerate(bounds):
-            v = slices[j] if cnt == n_rep else tail
+            v = slices[j % len(slices)] if cnt == n_rep else tail
             m.prep_init_device(v, vk, ctx, args.agg_id, enc_ap)
             parts.append(aggregate_to_tensor(m, args.agg_id, n_elems))
         job = fold_on_gpu(m, torch.cat(parts), len(parts), n_elems)
@@ -833,10 +843,13 @@ def main():
             "value": n_job * len(attrs) / wall,
             "unit": "report*prefix/s",
             "slices": len(bounds),
-            "what": "prep_init (leader) + fold of every resident report, %d slices of <= %d, slice agg shares "
+            "distinct_reports_resident": n_res,
+            "what": "prep_init (leader) + fold of every report of the job, %d slices of <= %d, slice agg shares "
                     "merged mod p on the GPU (mastic_fold_shares)" % (len(bounds), n_rep),
         }
-    out["config"]["resident_reports_per_rank"] = n_total
+    out["config"]["resident_reports_per_rank"] = n_res
+    (free_b, total_b) = torch.cuda.mem_get_info()
+    out["config"]["hbm_used_gb_after"] = (total_b - free_b) / 1e9
     out["config"]["shard_s"] = shard_s
 
     if rank == 0 and world == 1 and args.cpu_baseline:
