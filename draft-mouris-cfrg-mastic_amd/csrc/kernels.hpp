@@ -668,12 +668,17 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
 #endif
 #define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(EVAL_MIN_WAVES)))
 #define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16 + 16)
-// QUAD: payload refills of 2 blocks per sibling (4-block lockstep AES) instead
-// of 1 (paired); chosen at run time (mastic_ctx::eval_quad).  FC: the frontier
-// cache's last-level payload stores and parent indirection (AesArgs::last_w,
-// wp_by_node) are compiled in; the plain instantiation carries none of it
-// (the uniform branches cost 2.5 % at C2).
-template <class F, bool QUAD, bool FC>
+// GEN: the general level (the root level, which writes the root sum instead
+// of parent payload differences, and the last level, which emits the
+// truncated out shares, with their field multiplications for grouped
+// truncations); the interior levels (all others: 30 of C2's 32, 31 of C5's)
+// run an instantiation without that code, whose block loop then needs fewer
+// scalar registers (no spills of uniform flags into VGPR lanes).  FC: the
+// frontier cache's convert-seed staging, parent-payload recompute and fused
+// proofs are compiled in (only at a call's last level, so always with GEN);
+// the plain instantiation carries none of it (the uniform branches cost 2.5 %
+// at C2).
+template <class F, bool GEN, bool FC>
 __global__ __launch_bounds__(64 * EVAL_WAVES) EVAL_VGPR_ATTR
 void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
@@ -886,7 +891,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             pst(a.cs_out + (n1 + 4) * S, lb, tc1);
         }
         const int ce0 = a.child_exp[2 * pi], ce1 = a.child_exp[2 * pi + 1];
-        const int pf0 = a.child_pfx[2 * pi], pf1 = a.child_pfx[2 * pi + 1];
+        const int pf0 = GEN ? a.child_pfx[2 * pi] : -1, pf1 = GEN ? a.child_pfx[2 * pi + 1] : -1;
         const int row = 1 + p.output_len;
         E acc0 = F::zero(), acc1 = F::zero(), coef = F::from_u64(1);
         // Element e of both children: payload correction, frontier payloads,
@@ -897,7 +902,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             if (tc1) x1 = F::add(x1, cw);
             if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
             if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
-            if (l == 0) {
+            if (GEN && l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
                 // tiled (AbsorbArgs): word m of this group's 64 reports = one row
@@ -907,7 +912,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                     pst(payg + ((size_t)(pi * vl + e) * F::W32 + i) * a.bin_rstride, (uint32_t)lane * 4u,
                         F::word(d, i));
             }
-            if (pf0 >= 0 || pf1 >= 0) {
+            if (GEN && (pf0 >= 0 || pf1 >= 0)) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
                 if (e == 0) {
                     if (pf0 >= 0) pl_store<F>(a.out, pf0 * row, S, r, a.agg_id ? F::neg(x0) : x0);
@@ -944,7 +949,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         // waitcnt pass keeps a vmcnt wait in the loop header (every block)
         __builtin_amdgcn_s_waitcnt(0x0F70);
 #endif
-        if constexpr (!QUAD) {
+        {
             // Fast path: block b (counter b + 1) of each child's convert stream
             // holds Field64 candidates 2b and 2b + 1, or Field128 candidate b
             // (vdaf_poc next_vec after next(16)).  Speculate that no candidate
@@ -1006,10 +1011,10 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             // from the stream's start (a rejection shifts every later element)
             // up to e_hi, emitting from e_fast on; elements before it were
             // emitted by the fast path
-            typename EvalStream<F, QUAD>::type st0, st1;
+            typename EvalStream<F, false>::type st0, st1;
             st0.init(cs0);
             st1.init(cs1);
-            constexpr int G = EvalStream<F, QUAD>::type::GROUP;
+            constexpr int G = EvalStream<F, false>::type::GROUP;
             for (int e0 = 0; e0 < e_hi; e0 += G) {
                 asm volatile("" ::: "memory");
                 st0.refill(st1, e_hi - e0, TL, rkc);

@@ -774,7 +774,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // plain kernel (the variant's uniform branches and extra spills cost
         // a few per cent)
         if (lc && (hit || l == t->L || c->fc_all))
-            hipLaunchKernelGGL((k_eval_aes<F, false, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
+            hipLaunchKernelGGL((k_eval_aes<F, true, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
+                               p, pl, a);
+        else if (l == 0 || l == t->L)
+            hipLaunchKernelGGL((k_eval_aes<F, true, false>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
                                p, pl, a);
         else
             hipLaunchKernelGGL((k_eval_aes<F, false, false>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
@@ -1750,9 +1753,13 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
                             EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_eval_aes<F128, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_eval_aes<F64, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_eval_aes<F64, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_eval_aes<F128, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F64, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_absorb_pair, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess) {
