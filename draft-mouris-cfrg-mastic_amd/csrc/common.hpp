@@ -63,3 +63,6 @@ MH_D void pst(uint32_t* p, uint32_t lane_bytes, uint32_t v) {
 MH_D uint32_t pld_so(__amdgpu_buffer_rsrc_t rs, uint32_t lane_bytes, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(rs, lane_bytes, soff, MASTIC_SPONGE_LOAD_AUX);
 }
+MH_D void pst_so(__amdgpu_buffer_rsrc_t rs, uint32_t lane_bytes, uint32_t soff, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane_bytes, soff, 0);
+}

@@ -12,19 +12,36 @@
 #include "field.hpp"
 #include "params.hpp"
 
-// Element load/store on word planes.
-// plane0 and elt must be wave-uniform; r is the lane's report (column).
+// Element load/store on word planes: word i of element elt at
+// plane0 + (elt * W32 + i) * rowstride (rowstride = the plane stride, or the
+// tile row stride of the binder buffers).  plane0, elt and rowstride must be
+// wave-uniform; lane_bytes is the lane's byte offset in a row.  One buffer
+// descriptor per element and the word's row offset in soffset: a 4-word
+// Field128 element costs one descriptor (a few SALU) instead of one per word.
 template <class F>
-MH_D typename F::E pl_load(const uint32_t* plane0, int elt, int stride, int r) {
+MH_D typename F::E pl_load_rows(const uint32_t* plane0, int elt, int rowstride, uint32_t lane_bytes) {
+    const __amdgpu_buffer_rsrc_t rs = mh_rsrc(plane0 + (size_t)elt * F::W32 * rowstride);
+    const uint32_t rb = (uint32_t)rowstride * 4u;
     uint32_t w[F::W32];
 #pragma unroll
-    for (int i = 0; i < F::W32; i++) w[i] = pld(plane0 + (size_t)(elt * F::W32 + i) * stride, (uint32_t)r * 4u);
+    for (int i = 0; i < F::W32; i++) w[i] = pld_so(rs, lane_bytes, (uint32_t)i * rb);
     return F::from_words(w);
 }
 template <class F>
-MH_D void pl_store(uint32_t* plane0, int elt, int stride, int r, typename F::E x) {
+MH_D void pl_store_rows(uint32_t* plane0, int elt, int rowstride, uint32_t lane_bytes, typename F::E x) {
+    const __amdgpu_buffer_rsrc_t rs = mh_rsrc(plane0 + (size_t)elt * F::W32 * rowstride);
+    const uint32_t rb = (uint32_t)rowstride * 4u;
 #pragma unroll
-    for (int i = 0; i < F::W32; i++) pst(plane0 + (size_t)(elt * F::W32 + i) * stride, (uint32_t)r * 4u, F::word(x, i));
+    for (int i = 0; i < F::W32; i++) pst_so(rs, lane_bytes, (uint32_t)i * rb, F::word(x, i));
+}
+// r is the lane's report (column) of planes of stride `stride`
+template <class F>
+MH_D typename F::E pl_load(const uint32_t* plane0, int elt, int stride, int r) {
+    return pl_load_rows<F>(plane0, elt, stride, (uint32_t)r * 4u);
+}
+template <class F>
+MH_D void pl_store(uint32_t* plane0, int elt, int stride, int r, typename F::E x) {
+    pl_store_rows<F>(plane0, elt, stride, (uint32_t)r * 4u, x);
 }
 
 // Field constants needed by the FLP, computed once on the host.

@@ -906,11 +906,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
             } else {
                 // tiled (AbsorbArgs): word m of this group's 64 reports = one row
-                const E d = F::sub(F::sub(wp, x0), x1);
-#pragma unroll
-                for (int i = 0; i < F::W32; i++)
-                    pst(payg + ((size_t)(pi * vl + e) * F::W32 + i) * a.bin_rstride, (uint32_t)lane * 4u,
-                        F::word(d, i));
+                pl_store_rows<F>(payg, pi * vl + e, a.bin_rstride, (uint32_t)lane * 4u, F::sub(F::sub(wp, x0), x1));
             }
             if (GEN && (pf0 >= 0 || pf1 >= 0)) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
