@@ -295,7 +295,7 @@ class VirtualRanksMerge:
 
 
 def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None, warmup=None, n_job=None,
-              cpu_baseline=None, emit=True, m=None):
+              with_cpu=None, emit=True, m=None):
     """The reference's heavy-hitters driver (examples.py:37-91,
     mastic_amd.heavy_hitters) over HBM-resident reports: both aggregators'
     prep_init, the decide and the fold at every level, each level's agg shares
@@ -314,7 +314,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     split = args.split if split is None else split
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
-    do_cpu = args.cpu_baseline if cpu_baseline is None else cpu_baseline
+    do_cpu = args.cpu_baseline if with_cpu is None else with_cpu
     kw = dict(cfg["kw"])
     bits = kw.pop("bits")
     if m is None:
@@ -881,6 +881,7 @@ def main():
         }
         out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
+    ns = None
     if args.config == "c2" and args.north_star:
         # the north_star job (BASELINE.json): bit-exact prep_init + aggregate for
         # 1M reports x a full 32-bit prefix-level sweep, i.e. the reference's
@@ -892,8 +893,15 @@ def main():
         m = None
         gc.collect()
         ns_cfg = CONFIGS["c2sweep"]
-        ns = run_sweep(args, ns_cfg, world, rank, local, dist, torch, split=True, steps=1, warmup=1,
-                       n_job=ns_cfg["reports"], emit=False)
+        try:
+            ns = run_sweep(args, ns_cfg, world, rank, local, dist, torch, split=True, steps=1, warmup=1,
+                           n_job=ns_cfg["reports"], emit=False)
+        except Exception as e:  # keep the headline line; report the failed leg in it
+            import traceback
+            traceback.print_exc()
+            ns = None
+            out["north_star"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    if args.config == "c2" and args.north_star and ns is not None:
         nc = ns["config"]
         out["north_star"] = {
             "workload": nc["workload"],
