@@ -19,6 +19,8 @@ what is computed:
     RCCL all-gather + GPU mod-p fold), so each level's pruning decision is
     taken on the job-wide aggregate and all ranks walk the same frontier.
 """
+import time
+
 import numpy as np
 
 from .vdaf import Mastic
@@ -96,7 +98,8 @@ class SweepLevel:
 
 
 def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verify_key: bytes = None,
-                          trace=None, merge=None, timing=None, frontier_cache=None, cached_levels=None):
+                          trace=None, merge=None, timing=None, frontier_cache=None, cached_levels=None,
+                          phase_times=None):
     """poc/examples.py:37-91 on the GPU.
 
     ``reports`` is either the reference's list of
@@ -112,7 +115,17 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     (``Mastic.set_frontier_cache``): each level then evaluates only its new
     tree level when the previous level's tree is unchanged; if
     ``cached_levels`` is a list, the levels that took that path are appended.
+    If ``phase_times`` is a dict, the host wall time of each phase of a level
+    (enqueueing both prep_inits, decide, aggregate + merge, unshard + prune) is
+    accumulated into it (seconds).
     """
+    def clock(phase, t0):
+        if phase_times is not None:
+            t1 = time.perf_counter()
+            phase_times[phase] = phase_times.get(phase, 0.0) + t1 - t0
+            return t1
+        return t0
+
     if frontier_cache is not None:
         mastic.set_frontier_cache(frontier_cache)
     if verify_key is None:
@@ -150,6 +163,7 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
             merge.begin_level(level, prefixes)  # merges that need the level's candidates
         n_elems = len(prefixes) * (1 + mastic.OUTPUT_LEN) if device_merge else 0
         raw = agg_shares = None
+        tp = time.perf_counter() if phase_times is not None else 0.0
         if n and prefixes:
             # both aggregators' prep_init are queued before either result is
             # fetched, so the host work of the second overlaps the GPU run of
@@ -158,15 +172,18 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                 mastic.prep_init_device(dev, verify_key, ctx, agg_id, enc)
                 if cached_levels is not None and agg_id == 0 and frontier_cache and mastic.last_prep_was_cached():
                     cached_levels.append(level)
+            tp = clock("prep_init_enqueue", tp)
             if fast:
                 # both aggregators' prep_shares_to_prep + prep_next on the GPU:
                 # the prep shares stay in HBM, only the accept mask comes back
                 (accept, _codes) = mastic.decide_results(ctx, n)
                 alive &= accept == 1
+                tp = clock("decide_wait", tp)
                 if timing is not None:
                     for agg_id in range(2):
                         mastic.select_timing(agg_id)
                         timing.append(mastic.last_timing3())
+                tp = time.perf_counter() if phase_times is not None else 0.0
             else:
                 shares = []
                 for agg_id in range(2):
@@ -191,6 +208,7 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
             raw = [merge.total(n_elems, have_results=False)]  # same collectives on every rank
         else:
             agg_shares = [mastic.agg_init(agg_param) for _ in range(2)]
+        tp = clock("aggregate_merge", tp)
         if raw is not None:
             agg_result = _unshard_raw(mastic, raw, int(alive.sum()))
         else:
@@ -213,6 +231,7 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                         next_packed.append(_child_packed(packed[i], level + 1, True))
             prefixes = next_prefixes
             packed = next_packed
+            clock("unshard_prune", tp)
         else:
             for (prefix, count) in zip(prefixes, agg_result):
                 if count >= get_threshold(thresholds, prefix):
