@@ -897,13 +897,22 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         // Element e of both children: payload correction, frontier payloads,
         // the parent's payload difference (or the root sum), out shares.
         uint32_t* const payg = a.payload + (size_t)blockIdx.x * a.pay_gstride;  // tiled group
+#ifdef MASTIC_EXPERIMENT_KNOBS
+        // timing experiments (results wrong): 8 = no frontier-payload stores,
+        // 16 = no parent-payload loads, 32 = no payload-difference stores
+        const bool x_fr = !(a.dbg_skip & 8), x_diff = !(a.dbg_skip & 32);
+#else
+        constexpr bool x_fr = true, x_diff = true;
+#endif
         auto emit = [&](int e, E x0, E x1, E cw, E wp) {
             if (tc0) x0 = F::add(x0, cw);
             if (tc1) x1 = F::add(x1, cw);
-            if (ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
-            if (ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
+            if (x_fr && ce0 >= 0) pl_store<F>(a.fr_w_out, ce0 * vl + e, S, r, x0);
+            if (x_fr && ce1 >= 0) pl_store<F>(a.fr_w_out, ce1 * vl + e, S, r, x1);
             if (GEN && l == 0) {
                 pl_store<F>(pl.rootsum, e, S, r, F::add(x0, x1));
+            } else if (!x_diff) {
+                if (F::is_zero(F::sub(F::sub(wp, x0), x1))) a.out[0] = 0u;  // keep the work, drop the store
             } else {
                 // tiled (AbsorbArgs): word m of this group's 64 reports = one row
                 pl_store_rows<F>(payg, pi * vl + e, a.bin_rstride, (uint32_t)lane * 4u, F::sub(F::sub(wp, x0), x1));
@@ -937,7 +946,12 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         if constexpr (FC) wpb = a.recompute_wp ? a.wp_buf : a.fr_w_in;
         // level 0: the root's "parent payload" planes are zeroed by the host
         // (no branch, no zero-initialised registers in the block loop)
+#ifdef MASTIC_EXPERIMENT_KNOBS
+        const bool x_wp = !(a.dbg_skip & 16);
+        auto load_wp = [&](int e) { return x_wp ? pl_load<F>(wpb, pi * vl + e, S, r) : F::from_u64((uint64_t)e); };
+#else
         auto load_wp = [&](int e) { return pl_load<F>(wpb, pi * vl + e, S, r); };
+#endif
         int e_fast = e_lo;  // elements completed by the fast path
 #if MASTIC_EMIT_WAIT
         // the same before the block loop: the next parent's prefetched seed
