@@ -1444,17 +1444,35 @@ __global__ __launch_bounds__(256) void k_flp_query(McParams p, Planes pl, FlpCon
 
 // ------------------------------------------------------------- fold
 // agg_share[i] = sum over valid reports of out[i]  (agg_update + merge).
+// Workgroup (row, y) sums reports [y * chunk, (y + 1) * chunk) of one output
+// element into agg_words[y][row]; with gridDim.y > 1 the per-chunk partials
+// are then merged by k_fold_shares.  Four independent accumulators keep four
+// loads in flight per lane (a level of a sweep has few rows and ~1M reports:
+// one workgroup per row walking all reports was load-latency bound, ~7 ms).
 template <class F>
-__global__ __launch_bounds__(256) void k_fold(const uint32_t* out, int n, int stride, const uint8_t* valid,
+__global__ __launch_bounds__(256) void k_fold(const uint32_t* out, int n, int stride, const uint8_t* valid, int chunk,
                                               uint32_t* agg_words) {
     typedef typename F::E E;
     __shared__ E red[256];
     const int row = blockIdx.x;
-    E acc = F::zero();
-    for (int r = threadIdx.x; r < n; r += 256) {
-        if (valid && !valid[r]) continue;
-        acc = F::add(acc, pl_load<F>(out, row, stride, r));
+    const int r0 = blockIdx.y * chunk;
+    const int r1 = min(n, r0 + chunk);
+    auto get = [&](int r) {
+        const E x = pl_load<F>(out, row, stride, r);
+        return (valid && !valid[r]) ? F::zero() : x;
+    };
+    E a0 = F::zero(), a1 = F::zero(), a2 = F::zero(), a3 = F::zero();
+    int r = r0 + (int)threadIdx.x;
+    for (; r + 768 < r1; r += 1024) {
+        const E x0 = get(r), x1 = get(r + 256), x2 = get(r + 512), x3 = get(r + 768);
+        a0 = F::add(a0, x0);
+        a1 = F::add(a1, x1);
+        a2 = F::add(a2, x2);
+        a3 = F::add(a3, x3);
     }
+    for (; r < r1; r += 256) a0 = F::add(a0, get(r));
+    const E acc = F::add(F::add(a0, a1), F::add(a2, a3));
+    agg_words += (size_t)blockIdx.y * gridDim.x * F::W32;
     red[threadIdx.x] = acc;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {

@@ -171,6 +171,7 @@ struct mastic_ctx {
     DevBuf pfx_bytes, pfx_meta;
     DevBuf consts;   // alpha^-i table for prove
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
+    DevBuf agg_part;            // per-chunk partial sums of a split fold (aggregate_impl)
     DevBuf stage;               // result encoding / decide staging
     bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
@@ -1259,13 +1260,38 @@ static int aggregate_impl(mastic_ctx* c, int agg_id, const uint8_t* valid, uint3
         HIPCHK(c, hipMemcpyAsync(c->agg_valid.p, valid, R.n, hipMemcpyHostToDevice, c->stream));
         dv = c->agg_valid.as<uint8_t>();
     }
-    if (rows) {
+    if (!rows) return 0;
+    // few rows over many reports (a sweep level: ~700 rows x 1M reports):
+    // split the reports into chunks so the grid fills the chip, then merge
+    // the chunks' partial sums mod p (k_fold_shares)
+    const size_t target = (size_t)c->n_cus * 16;
+    size_t chunks = 1;
+    if (rows < target && R.n >= 8192)
+        chunks = std::min<size_t>({(target + rows - 1) / rows, R.n / 4096, (size_t)1024});
+    const size_t chunk = chunks > 1 ? round_up((R.n + chunks - 1) / chunks, 256) : R.n;
+    chunks = (R.n + chunk - 1) / chunk;
+    uint32_t* dst = dagg;
+    if (chunks > 1) {
+        if (!c->agg_part.ensure(std::max<size_t>(chunks * rows * p.w32 * 4, (size_t)1 << 20)))
+            return fail(c, MASTIC_ENOMEM, "out of device memory");
+        dst = c->agg_part.as<uint32_t>();
+    }
+    const dim3 grid((unsigned)rows, (unsigned)chunks);
+    if (p.field == 64)
+        hipLaunchKernelGGL(k_fold<F64>, grid, dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n, (int)R.stride,
+                           dv, (int)chunk, dst);
+    else
+        hipLaunchKernelGGL(k_fold<F128>, grid, dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n, (int)R.stride,
+                           dv, (int)chunk, dst);
+    HIPCHK(c, hipGetLastError());
+    if (chunks > 1) {
+        const dim3 g2((unsigned)((rows + 255) / 256));
         if (p.field == 64)
-            hipLaunchKernelGGL(k_fold<F64>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
-                               (int)R.stride, dv, dagg);
+            hipLaunchKernelGGL(k_fold_shares<F64>, g2, dim3(256), 0, c->stream, (const uint32_t*)dst, (int)chunks,
+                               (int)rows, dagg);
         else
-            hipLaunchKernelGGL(k_fold<F128>, dim3(rows), dim3(256), 0, c->stream, R.out.as<uint32_t>(), (int)R.n,
-                               (int)R.stride, dv, dagg);
+            hipLaunchKernelGGL(k_fold_shares<F128>, g2, dim3(256), 0, c->stream, (const uint32_t*)dst, (int)chunks,
+                               (int)rows, dagg);
         HIPCHK(c, hipGetLastError());
     }
     return 0;

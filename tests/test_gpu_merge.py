@@ -215,3 +215,48 @@ def test_aggregate_device_waits_for_callers_stream(torch_cuda):
         out.fill_(0xA5)
         aggregate_to_tensor(m, 0, n_elems, out=out)
         assert out.cpu().numpy().tobytes() == want
+
+
+@pytest.mark.parametrize("circuit,kw,n", [("Count", dict(bits=8), 20000),
+                                          ("Histogram", dict(bits=6, length=3, chunk_length=2), 9000)],
+                         ids=["Field64", "Field128"])
+def test_aggregate_split_fold_matches_field_sum(torch_cuda, circuit, kw, n):
+    """agg_update over many reports and few output elements (a sweep level)
+    runs as a report-chunked fold plus a mod-p merge of the chunk partials
+    (aggregate_impl); it equals the field sum of the out shares of the valid
+    reports (mastic.py:384-388), with and without a validity mask."""
+    import numpy as np
+    import mastic_amd
+    kw = dict(kw)
+    bits = kw.pop("bits")
+    m = mastic_amd.Mastic(bits, circuit, **kw)
+    rng = random.Random(n + bits)
+    ctx = b"split-fold"
+    vals = [rng.randrange(2 ** bits) for _ in range(n)]
+    alphas = b"".join((v << (8 - bits)).to_bytes(1, "big") for v in vals)
+    if circuit == "Count":
+        meas = [rng.randrange(2) for _ in range(n)]
+    else:
+        meas = [rng.randrange(kw["length"]) for _ in range(n)]
+    betas = b"".join(m.field.encode_vec(m.encode_measurement(x)) for x in meas)
+    dev = m.reports_shard(ctx, alphas, betas, rng.randbytes(16 * n), rng.randbytes(m.RAND_SIZE * n))
+    cand = tuple(sorted(set(tuple(bool((v >> (bits - 1 - i)) & 1) for i in range(3)) for v in vals[:50])))
+    enc = m.encode_agg_param((2, cand, True))
+    vk = bytes(range(16))
+    p = m.field.MODULUS
+    enc_sz = m.field.ENCODED_SIZE
+    rows = len(cand) * (1 + m.OUTPUT_LEN)
+    valid = np.array([rng.random() < 0.8 for _ in range(n)], dtype=np.uint8)
+    for agg_id in range(2):
+        m.prep_init_device(dev, vk, ctx, agg_id, enc)
+        (_ps, _js, out, st) = m.prep_result(dev, agg_id, enc, want_out_shares=True)
+        assert list(st) == [0] * n
+        el = [int.from_bytes(out[i:i + enc_sz], "little") for i in range(0, len(out), enc_sz)]
+        per = [el[r * rows:(r + 1) * rows] for r in range(n)]
+        for mask in (None, valid):
+            want = [0] * rows
+            for r in range(n):
+                if mask is None or mask[r]:
+                    want = [a + b for (a, b) in zip(want, per[r])]
+            want = b"".join((w % p).to_bytes(enc_sz, "little") for w in want)
+            assert m.aggregate_device(agg_id, enc, mask, raw=True) == want
