@@ -555,6 +555,18 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
                 jobs.append((spec, enc_ap, rn[16 * i:16 * (i + 1)], pub[ps * i:ps * (i + 1)],
                              in0[isz * i:isz * (i + 1)], vk, ctx, 0))
         wall, res = cpu_baseline(jobs, procs)
+        # the same reports at the same levels through the GPU path (leader
+        # prep_init of the resident reports with the sweep's candidate lists):
+        # the oracle replays part of the timed workload bit for bit
+        m.set_frontier_cache(False)
+        gpu_ps = []
+        for lv in lvls:
+            enc_ap = m.encode_agg_param((lv.level, tuple(lv.prefixes), lv.level == 0))
+            (gps, _js, _o, _st) = m.prep_init_batch(vk, ctx, 0, enc_ap, rn[:16 * procs], pub[:ps * procs],
+                                                    in0[:isz * procs], want_out_shares=False)
+            psz = m.prep_share_size(lv.level == 0)
+            gpu_ps.append([gps[psz * i:psz * (i + 1)] for i in range(procs)])
+        parity = all(res[i * len(lvls) + k][1] == gpu_ps[k][i] for i in range(procs) for k in range(len(lvls)))
         cu = procs * sum(len(lv.prefixes) for lv in lvls)
         out["cpu_baseline"] = {
             "value": cu / wall,
@@ -564,9 +576,11 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             "single_process_value": cu / sum(r[0] for r in res),
             "sample": "%d reports (one per process, spawn pool of %d) x leader prep_init at levels %s of the "
                       "sweep with the GPU run's candidate prefixes; poc-faithful Python oracle with C "
-                      "AES/TurboSHAKE" % (procs, procs, [lv.level for lv in lvls]),
+                      "AES/TurboSHAKE; GPU/CPU prep shares bit-identical: %s" % (
+                          procs, procs, [lv.level for lv in lvls], parity),
         }
         out["cpu_baseline"].update(cpu_host_info())
+        out["cpu_parity"] = parity
     del reps
     if rank == 0 and emit:
         print(json.dumps(out))
@@ -936,6 +950,7 @@ def main():
             cb = ns["cpu_baseline"]
             out["north_star"]["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind",
                                                                     "single_process_value", "sample")}
+            out["north_star"]["cpu_parity"] = ns.get("cpu_parity")
             out["north_star"]["speedup_vs_cpu_pool"] = ns["value"] / cb["value"]
             out["north_star"]["speedup_vs_cpu_core"] = ns["value"] / cb["single_process_value"]
     if rank == 0:
