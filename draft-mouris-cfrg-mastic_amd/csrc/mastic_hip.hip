@@ -923,7 +923,15 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         d.p = nullptr;
         d.bytes = 0;
         d.own = true;
-        return d.ensure(std::max(want, old + old / 2)) || d.ensure(want);
+        if (d.ensure(std::max(want, old + old / 2)) || d.ensure(want)) return true;
+        // HBM is held by the work arena (sized to the budget when the results
+        // were smaller) and by retired buffers: once the queued work is done,
+        // free both and retry; the arena is re-allocated below, within what is
+        // left (a 2M-report sweep's out shares reach 32 GB per aggregator)
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+        c->bury();
+        c->work.release();
+        return d.ensure(want);
     };
     if (!rgrow(R.eval_proof, S * 8 * 4) || !rgrow(R.status, S * 4) ||
         !rgrow(R.out, S * 4 * std::max<size_t>(1, (size_t)t->n_prefixes * (1 + p.output_len) * p.w32)) ||
