@@ -377,8 +377,10 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
                                      timing=timing, frontier_cache=bool(args.frontier_cache),
                                      cached_levels=cached_levels, phase_times=phases if timing is not None else None)
 
-    for _ in range(warmup):
+    for i in range(warmup):
         step(None, None)
+        if rank == 0:
+            print("[sweep] warmup %d done" % (i + 1), file=sys.stderr, flush=True)
     m.synchronize()
     if dist:
         dist.barrier()
@@ -386,10 +388,12 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     t0 = time.perf_counter()
     traces, timing = [], []
     hh = None
-    for _ in range(steps):
+    for i in range(steps):
         tr = []
         hh = step(tr, timing)
         traces.append(tr)
+        if rank == 0:
+            print("[sweep] step %d done" % (i + 1), file=sys.stderr, flush=True)
     m.synchronize()
     torch.cuda.synchronize()
     if dist:
@@ -840,10 +844,15 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         parts = []
+        t_last = t1
         for (j, (first, cnt)) in enumerate(bounds):
             v = slices[j % len(slices)] if cnt == n_rep else tail
             m.prep_init_device(v, vk, ctx, args.agg_id, enc_ap)
             parts.append(aggregate_to_tensor(m, args.agg_id, n_elems))
+            if rank == 0 and time.perf_counter() - t_last > 30:  # progress for long jobs (C4/C5 sizes)
+                t_last = time.perf_counter()
+                print("[full_job] %d / %d slices, %.0f s" % (j + 1, len(bounds), t_last - t1), file=sys.stderr,
+                      flush=True)
         job = fold_on_gpu(m, torch.cat(parts), len(parts), n_elems)
         if world > 1:
             job = merge_agg_shares(m, job, dist)
