@@ -1276,8 +1276,9 @@ static int aggregate_impl(mastic_ctx* c, int agg_id, const uint8_t* valid, uint3
     size_t chunks = 1;
     if (rows < target && R.n >= 8192)
         chunks = std::min<size_t>({(target + rows - 1) / rows, R.n / 4096, (size_t)1024});
-    const size_t chunk = chunks > 1 ? round_up((R.n + chunks - 1) / chunks, 256) : R.n;
-    chunks = (R.n + chunk - 1) / chunk;
+    // (an empty batch still writes its all-zero agg share: one chunk)
+    const size_t chunk = chunks > 1 ? round_up((R.n + chunks - 1) / chunks, 256) : std::max<size_t>(R.n, 1);
+    chunks = std::max<size_t>(1, (R.n + chunk - 1) / chunk);
     uint32_t* dst = dagg;
     if (chunks > 1) {
         if (!c->agg_part.ensure(std::max<size_t>(chunks * rows * p.w32 * 4, (size_t)1 << 20)))
