@@ -713,93 +713,6 @@ MH_D void ctr_blocks_pf2(const AesPerm& T, const RK& rk, const AesCtrGroup* cons
     }
 }
 
-// The extend pair (counters 0 and 1 of ONE seed) for ctr_blocks_l2: the
-// group of that seed plus rounds 1-2 of both counters looked up inside the
-// init's two batches (17 and 20 reads) instead of two more round trips.
-template <class RK>
-MH_D void ctr_group_init_pair(const AesPerm& T, const RK& rk, const uint32_t* seed, AesCtrGroup& g,
-                              uint32_t (&l2)[8]) {
-    const uint4 k0 = rk(0), k1 = rk(1), k2 = rk(2);
-    const uint32_t a0 = seed[2] ^ k0.x, a1 = seed[3] ^ k0.y;
-    const uint32_t a2 = seed[2] ^ seed[0] ^ k0.z, a3 = seed[3] ^ seed[1] ^ k0.w;  // counter bits above 7: 0
-    uint32_t l[17];
-    l[0] = lds_read_asm(T.a0<0>(a0));
-    l[1] = lds_read_asm(T.a1<1>(a1));
-    l[2] = lds_read_asm(T.a2<2>(a2));
-    l[3] = lds_read_asm(T.a3<3>(a3));
-    l[4] = lds_read_asm(T.a0<0>(a1));
-    l[5] = lds_read_asm(T.a1<1>(a2));
-    l[6] = lds_read_asm(T.a2<2>(a3));
-    l[7] = lds_read_asm(T.a3<3>(a0));
-    l[8] = lds_read_asm(T.a1<1>(a3));
-    l[9] = lds_read_asm(T.a2<2>(a0));
-    l[10] = lds_read_asm(T.a3<3>(a1));
-    l[11] = lds_read_asm(T.a0<0>(a3));
-    l[12] = lds_read_asm(T.a1<1>(a0));
-    l[13] = lds_read_asm(T.a2<2>(a1));
-    l[14] = lds_read_asm(T.a3<3>(a2));
-    const uint32_t ga = T.a0<0>(a2);
-    l[15] = lds_read_asm(ga);             // round 1, counter 0
-    l[16] = lds_read_asm(ga ^ (1u << 8));  // round 1, counter 1
-    asm volatile("s_waitcnt lgkmcnt(0)" : MH_PIN16(l, 0), "+v"(l[16]));
-    const uint32_t t0 = xor3_u32(xor3_u32(l[0], l[1], l[2]), l[3], k1.x);
-    const uint32_t t1 = xor3_u32(xor3_u32(l[4], l[5], l[6]), l[7], k1.y);
-    const uint32_t t3 = xor3_u32(xor3_u32(l[11], l[12], l[13]), l[14], k1.w);
-    g.p2 = xor3_u32(l[8], l[9], l[10]) ^ k1.z;
-    g.a = ga;
-    uint32_t m[20];
-    m[0] = lds_read_asm(T.a0<0>(t0));
-    m[1] = lds_read_asm(T.a1<1>(t1));
-    m[2] = lds_read_asm(T.a3<3>(t3));
-    m[3] = lds_read_asm(T.a0<0>(t1));
-    m[4] = lds_read_asm(T.a2<2>(t3));
-    m[5] = lds_read_asm(T.a3<3>(t0));
-    m[6] = lds_read_asm(T.a1<1>(t3));
-    m[7] = lds_read_asm(T.a2<2>(t0));
-    m[8] = lds_read_asm(T.a3<3>(t1));
-    m[9] = lds_read_asm(T.a0<0>(t3));
-    m[10] = lds_read_asm(T.a1<1>(t0));
-    m[11] = lds_read_asm(T.a2<2>(t1));
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t u2 = g.p2 ^ l[15 + j];
-        m[12 + 4 * j + 0] = lds_read_asm(T.a2<2>(u2));
-        m[12 + 4 * j + 1] = lds_read_asm(T.a1<1>(u2));
-        m[12 + 4 * j + 2] = lds_read_asm(T.a0<0>(u2));
-        m[12 + 4 * j + 3] = lds_read_asm(T.a3<3>(u2));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : MH_PIN16(m, 0), "+v"(m[16]), "+v"(m[17]), "+v"(m[18]), "+v"(m[19]));
-    g.q[0] = xor3_u32(m[0], m[1], m[2]) ^ k2.x;
-    g.q[1] = xor3_u32(m[3], m[4], m[5]) ^ k2.y;
-    g.q[2] = xor3_u32(m[6], m[7], m[8]) ^ k2.z;
-    g.q[3] = xor3_u32(m[9], m[10], m[11]) ^ k2.w;
-#pragma unroll
-    for (int i = 0; i < 8; i++) l2[i] = m[12 + i];
-}
-
-// ctr_blocks_n<2> from round 3 on, rounds 1-2 looked up ahead (l2), no lookahead.
-template <class RK>
-MH_D void ctr_blocks_l2(const AesPerm& T, const RK& rk, const AesCtrGroup* const (&g)[2],
-                        const uint32_t* const (&seed)[2], const uint32_t (&ctr)[2], const uint32_t (&l2)[8],
-                        uint32_t* const (&out)[2]) {
-    uint32_t x[2][4];
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) x[j][c] = g[j]->q[c] ^ l2[4 * j + c];
-#pragma unroll
-    for (int r = 3; r < 10; r++) aes_round_n<2>(T, x, rk(r));
-    aes_last_n<2>(T, x, rk(10));
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t* sd = seed[j];
-        out[j][0] = x[j][0] ^ sd[2];
-        out[j][1] = x[j][1] ^ sd[3];
-        out[j][2] = xor3_u32(x[j][2], sd[2] ^ sd[0], ctr[j]);
-        out[j][3] = xor3_u32(x[j][3], sd[3], sd[1]);
-    }
-}
-
 // Round 1's varying lookup of two blocks (ctr_blocks_pf's l1), with its own wait.
 MH_D void ctr_round1(const AesCtrGroup* const (&g)[2], const uint32_t (&ctr)[2], uint32_t (&l1)[2]) {
 #pragma unroll

@@ -834,13 +834,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             const uint32_t* const sd2[2] = {ps, ps};
             const uint32_t cv[2] = {0u, 1u};
             uint32_t* const ov[2] = {cs0, cs1};
-#if MASTIC_PREFETCH_R1 >= 2
-            // the init also looks up rounds 1-2 of counters 0 and 1
-            uint32_t l2e[8];
-            ctr_group_init_pair(TL, rke, ps, gp, l2e);
-            (void)gi;
-            ctr_blocks_l2(TL, rke, gg, sd2, cv, l2e, ov);
-#elif MASTIC_PREFETCH_R1
+#if MASTIC_PREFETCH_R1
             // the init also looks up round 1 of counters 0 and 1
             uint32_t e0[1], e1[1];
             ctr_group_init<1>(TL, rke, sd, ch, gi, e0, e1);
