@@ -445,13 +445,10 @@ struct AesCtrGroup {
 // round 1's varying byte for the group's first counter (ctr_hi | 0), returned
 // in l1[j]: ctr_blocks_pf's l1 for that counter without a round trip of its
 // own; with l1b != nullptr the second batch does the same for counter
-// ctr_hi | 1 (the extend pair: counters 0 and 1 of one seed); with l2 !=
-// nullptr (and l1) the second batch's free slots 12-15 look up round 2 of the
-// first counter (ctr_blocks_pf2's l2, 4 words per group).
+// ctr_hi | 1 (the extend pair: counters 0 and 1 of one seed).
 template <int N, class RK>
 MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (&seed)[N], const uint32_t (&ctr_hi)[N],
-                         AesCtrGroup* const (&g)[N], uint32_t* l1 = nullptr, uint32_t* l1b = nullptr,
-                         uint32_t* l2 = nullptr) {
+                         AesCtrGroup* const (&g)[N], uint32_t* l1 = nullptr, uint32_t* l1b = nullptr) {
     static_assert(N == 1 || N == 2, "N = 1 or 2");
     const uint4 k0 = rk(0), k1 = rk(1), k2 = rk(2);
     uint32_t L[16 * N];  // 15 used per group
@@ -515,28 +512,14 @@ MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (
         m[9] = lds_read_asm(T.a0<0>(t3));
         m[10] = lds_read_asm(T.a1<1>(t0));
         m[11] = lds_read_asm(T.a2<2>(t1));
-        if (l2) {
-            const uint32_t u2 = g[j]->p2 ^ L[16 * j + 15];  // round 1 of the first counter, from batch 1
-            m[12] = lds_read_asm(T.a2<2>(u2));
-            m[13] = lds_read_asm(T.a1<1>(u2));
-            m[14] = lds_read_asm(T.a0<0>(u2));
-            m[15] = lds_read_asm(T.a3<3>(u2));
-        } else {
-            m[12] = l1b ? lds_read_asm(g[j]->a ^ (1u << 8)) : 0u;
+        m[12] = l1b ? lds_read_asm(g[j]->a ^ (1u << 8)) : 0u;
 #pragma unroll
-            for (int i = 13; i < 16; i++) m[i] = 0u;
-        }
+        for (int i = 13; i < 16; i++) m[i] = 0u;
     }
     aes_pin<N>(M);
     if (l1b) {
 #pragma unroll
         for (int j = 0; j < N; j++) l1b[j] = M[16 * j + 12];
-    }
-    if (l2) {
-#pragma unroll
-        for (int j = 0; j < N; j++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) l2[4 * j + i] = M[16 * j + 12 + i];
     }
 #pragma unroll
     for (int j = 0; j < N; j++) {
@@ -633,76 +616,6 @@ MH_D void ctr_blocks_pf(const AesPerm& T, const RK& rk, const AesCtrGroup* const
 #pragma unroll
     for (int r = 4; r < 10; r++) aes_round_n<2>(T, x, rk(r));
     aes_last_n<2>(T, x, rk(10));
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t* sd = seed[j];
-        out[j][0] = x[j][0] ^ sd[2];
-        out[j][1] = x[j][1] ^ sd[3];
-        out[j][2] = xor3_u32(x[j][2], sd[2] ^ sd[0], ctr[j]);
-        out[j][3] = xor3_u32(x[j][3], sd[3], sd[1]);
-    }
-}
-
-// aes_last_n<2> plus 8 extra reads (addresses xa, results xo) covered by its wait.
-MH_D void aes_last2_x8(const AesPerm& T, uint32_t (&s)[2][4], uint4 k, const uint32_t (&xa)[8], uint32_t (&xo)[8]) {
-    uint32_t L[32];
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            L[16 * j + 4 * c + 0] = lds_read_asm(T.a0<0>(s[j][c]));
-            L[16 * j + 4 * c + 1] = lds_read_asm(T.a0<1>(s[j][(c + 1) & 3]));
-            L[16 * j + 4 * c + 2] = lds_read_asm(T.a0<2>(s[j][(c + 2) & 3]));
-            L[16 * j + 4 * c + 3] = lds_read_asm(T.a0<3>(s[j][(c + 3) & 3]));
-        }
-#pragma unroll
-    for (int e = 0; e < 8; e++) xo[e] = lds_read_asm(xa[e]);
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : MH_PIN16(L, 0), MH_PIN16(L, 16), "+v"(xo[0]), "+v"(xo[1]), "+v"(xo[2]), "+v"(xo[3]), "+v"(xo[4]),
-                   "+v"(xo[5]), "+v"(xo[6]), "+v"(xo[7]));
-    const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const uint32_t* q = L + 16 * j + 4 * c;
-            const uint32_t lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0501u);
-            const uint32_t hi = __builtin_amdgcn_perm(q[3], q[2], 0x05010c0cu);
-            s[j][c] = xor3_u32(lo, hi, kk[c]);
-        }
-}
-
-// ctr_blocks_n<2> from round 3 on: the pair's rounds 1-2 were looked up ahead
-// (l2: round 2's four lookups per block, by the group init or the previous
-// pair), and this pair looks up the NEXT pair's round 1 with its round 3
-// (addresses pa1) and the next pair's round 2 with its last round (from the
-// next pair's groups' p2 values p2n): 8 LDS round trips per pair instead of
-// 10.  The lookahead values are garbage when the next pair starts a new group
-// (the caller re-initialises, which looks them up again).
-template <class RK>
-MH_D void ctr_blocks_pf2(const AesPerm& T, const RK& rk, const AesCtrGroup* const (&g)[2],
-                         const uint32_t* const (&seed)[2], const uint32_t (&ctr)[2], const uint32_t (&l2)[8],
-                         const uint32_t (&pa1)[2], const uint32_t (&p2n)[2], uint32_t (&l2_next)[8],
-                         uint32_t* const (&out)[2]) {
-    uint32_t x[2][4];
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) x[j][c] = g[j]->q[c] ^ l2[4 * j + c];
-    uint32_t l1n[2];
-    aes_round_n_x<2, 2>(T, x, rk(3), pa1, l1n);
-#pragma unroll
-    for (int r = 4; r < 10; r++) aes_round_n<2>(T, x, rk(r));
-    uint32_t xa[8];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t u2 = p2n[j] ^ l1n[j];
-        xa[4 * j + 0] = T.a2<2>(u2);
-        xa[4 * j + 1] = T.a1<1>(u2);
-        xa[4 * j + 2] = T.a0<0>(u2);
-        xa[4 * j + 3] = T.a3<3>(u2);
-    }
-    aes_last2_x8(T, x, rk(10), xa, l2_next);
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const uint32_t* sd = seed[j];

@@ -868,19 +868,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         AesCtrGroup g0, g1;
         uint32_t g_hi = 0;  // counter bits above 7 of the groups (uniform)
         const uint32_t* const csd[2] = {cs0, cs1};
-#if MASTIC_PREFETCH_R1 >= 2
-        // rounds 1-2 of the next block pair are looked up ahead
-        // (ctr_blocks_pf2): a group init returns them for its first counter,
-        // every pair looks them up for the following one
-        uint32_t l2[8];
-        auto init_groups = [&](uint32_t hi) {
-            const uint32_t ch2[2] = {hi, hi};
-            AesCtrGroup* const gi[2] = {&g0, &g1};
-            uint32_t l1i[2];
-            ctr_group_init<2>(TL, rkc, csd, ch2, gi, l1i, nullptr, l2);
-            g_hi = hi;
-        };
-#elif MASTIC_PREFETCH_R1
+#if MASTIC_PREFETCH_R1
         // round 1's varying lookup of the next block pair (ctr_blocks_pf): a
         // group init returns it for its first counter, every pair prefetches
         // it for the following one
@@ -906,15 +894,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         {
             const uint32_t cv[2] = {0u, 0u};
             uint32_t* const ov[2] = {ns0, ns1};
-#if MASTIC_PREFETCH_R1 >= 2
-            // the next seed (counter 0) looks up rounds 1-2 of payload block 0 (counter 1)
-            const uint32_t pa1[2] = {g0.a ^ (1u << 8), g1.a ^ (1u << 8)};
-            const uint32_t p2n[2] = {g0.p2, g1.p2};
-            uint32_t l2n[8];
-            ctr_blocks_pf2(TL, rkc, gg, csd, cv, l2, pa1, p2n, l2n, ov);
-#pragma unroll
-            for (int i = 0; i < 8; i++) l2[i] = l2n[i];
-#elif MASTIC_PREFETCH_R1
+#if MASTIC_PREFETCH_R1
             // the next seed (counter 0) prefetches payload block 0's (counter 1)
             const uint32_t pa[2] = {g0.a ^ (1u << 8), g1.a ^ (1u << 8)};
             uint32_t l1n[2];
@@ -1042,23 +1022,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                     wpb = load_wp(e1);
                 }
                 uint32_t o0[4], o1[4];
-#if MASTIC_CTR_GROUPS && MASTIC_PREFETCH_R1 >= 2
-                {
-                    // rounds 1-2 of this pair were looked up by the previous
-                    // pair, or by the group init when a group starts here
-                    const uint32_t c = (uint32_t)(b + 1);
-                    if ((c & ~0xffu) != g_hi) init_groups(c & ~0xffu);
-                    const uint32_t cv[2] = {c, c};
-                    const uint32_t cn = (c + 1) & 0xffu;  // the next pair's counter, low byte
-                    const uint32_t pa1[2] = {g0.a ^ (cn << 8), g1.a ^ (cn << 8)};
-                    const uint32_t p2n[2] = {g0.p2, g1.p2};
-                    uint32_t l2n[8];
-                    uint32_t* const ov[2] = {o0, o1};
-                    ctr_blocks_pf2(TL, rkc, gg, csd, cv, l2, pa1, p2n, l2n, ov);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) l2[i] = l2n[i];
-                }
-#elif MASTIC_CTR_GROUPS && MASTIC_PREFETCH_R1
+#if MASTIC_CTR_GROUPS && MASTIC_PREFETCH_R1
                 {
                     // round 1 of this pair was looked up with the previous
                     // pair's round 3 (ctr_blocks_pf), unless a group starts here
