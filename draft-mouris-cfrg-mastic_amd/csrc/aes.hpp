@@ -443,12 +443,10 @@ struct AesCtrGroup {
 //
 // With l1 != nullptr the first batch's unused 16th read slot also looks up
 // round 1's varying byte for the group's first counter (ctr_hi | 0), returned
-// in l1[j]: ctr_blocks_pf's l1 for that counter without a round trip of its
-// own; with l1b != nullptr the second batch does the same for counter
-// ctr_hi | 1 (the extend pair: counters 0 and 1 of one seed).
+// in l1[j]: ctr_blocks_pf's l1 for that counter without a round trip of its own.
 template <int N, class RK>
 MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (&seed)[N], const uint32_t (&ctr_hi)[N],
-                         AesCtrGroup* const (&g)[N], uint32_t* l1 = nullptr, uint32_t* l1b = nullptr) {
+                         AesCtrGroup* const (&g)[N], uint32_t* l1 = nullptr) {
     static_assert(N == 1 || N == 2, "N = 1 or 2");
     const uint4 k0 = rk(0), k1 = rk(1), k2 = rk(2);
     uint32_t L[16 * N];  // 15 used per group
@@ -512,15 +510,10 @@ MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (
         m[9] = lds_read_asm(T.a0<0>(t3));
         m[10] = lds_read_asm(T.a1<1>(t0));
         m[11] = lds_read_asm(T.a2<2>(t1));
-        m[12] = l1b ? lds_read_asm(g[j]->a ^ (1u << 8)) : 0u;
 #pragma unroll
-        for (int i = 13; i < 16; i++) m[i] = 0u;
+        for (int i = 12; i < 16; i++) m[i] = 0u;
     }
     aes_pin<N>(M);
-    if (l1b) {
-#pragma unroll
-        for (int j = 0; j < N; j++) l1b[j] = M[16 * j + 12];
-    }
 #pragma unroll
     for (int j = 0; j < N; j++) {
         const uint32_t* m = M + 16 * j;

@@ -830,22 +830,12 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             const uint32_t* const sd[1] = {ps};
             const uint32_t ch[1] = {0u};
             AesCtrGroup* const gi[1] = {&gp};
+            ctr_group_init<1>(TL, rke, sd, ch, gi);
             const AesCtrGroup* const gg[2] = {&gp, &gp};
             const uint32_t* const sd2[2] = {ps, ps};
             const uint32_t cv[2] = {0u, 1u};
             uint32_t* const ov[2] = {cs0, cs1};
-#if MASTIC_PREFETCH_R1
-            // the init also looks up round 1 of counters 0 and 1
-            uint32_t e0[1], e1[1];
-            ctr_group_init<1>(TL, rke, sd, ch, gi, e0, e1);
-            const uint32_t l1e[2] = {e0[0], e1[0]};
-            const uint32_t pa[2] = {gp.a, gp.a};  // nothing to prefetch: the convert seeds depend on this
-            uint32_t unused[2];
-            ctr_blocks_pf(TL, rke, gg, sd2, cv, l1e, pa, unused, ov);
-#else
-            ctr_group_init<1>(TL, rke, sd, ch, gi);
             ctr_blocks_n<2>(TL, rke, gg, sd2, cv, ov);
-#endif
         }
 #else
         fixed_key_block2(TL, rke, ps, 0u, ps, 1u, cs0, cs1);
