@@ -326,36 +326,6 @@ MH_D void aes_round_n(const AesPerm& T, uint32_t (&s)[N][4], uint4 k) {
         }
 }
 
-// aes_round_n plus E extra table reads (addresses xa, results xo) issued with
-// the round's lookups and covered by its one wait: a read whose address does
-// not depend on this round (the next block's round-1 lookup, ctr_blocks_pf)
-// rides along instead of costing an LDS round trip of its own.
-template <int N, int E>
-MH_D void aes_round_n_x(const AesPerm& T, uint32_t (&s)[N][4], uint4 k, const uint32_t (&xa)[E], uint32_t (&xo)[E]) {
-    static_assert(N == 2 && E == 2, "N = 2 blocks, 2 extra reads");
-    uint32_t L[16 * N];
-#pragma unroll
-    for (int j = 0; j < N; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            L[16 * j + 4 * c + 0] = lds_read_asm(T.a0<0>(s[j][c]));
-            L[16 * j + 4 * c + 1] = lds_read_asm(T.a1<1>(s[j][(c + 1) & 3]));
-            L[16 * j + 4 * c + 2] = lds_read_asm(T.a2<2>(s[j][(c + 2) & 3]));
-            L[16 * j + 4 * c + 3] = lds_read_asm(T.a3<3>(s[j][(c + 3) & 3]));
-        }
-    xo[0] = lds_read_asm(xa[0]);
-    xo[1] = lds_read_asm(xa[1]);
-    asm volatile("s_waitcnt lgkmcnt(0)" : MH_PIN16(L, 0), MH_PIN16(L, 16), "+v"(xo[0]), "+v"(xo[1]));
-    const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
-#pragma unroll
-    for (int j = 0; j < N; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const uint32_t* q = L + 16 * j + 4 * c;
-            s[j][c] = xor3_u32(xor3_u32(q[0], q[1], q[2]), q[3], kk[c]);
-        }
-}
-
 // Final round of N blocks: S-box bytes (byte 1 of the T0 entries) packed with
 // two v_perm_b32 and merged with the round key by one xor3.
 template <int N>
@@ -440,13 +410,9 @@ struct AesCtrGroup {
 
 // The shared part of N groups (seeds seed[j], counters ctr_hi[j] & ~0xff) in
 // lockstep: 15 round-1 and 12 round-2 lookups per group.
-//
-// With l1 != nullptr the first batch's unused 16th read slot also looks up
-// round 1's varying byte for the group's first counter (ctr_hi | 0), returned
-// in l1[j]: ctr_blocks_pf's l1 for that counter without a round trip of its own.
 template <int N, class RK>
 MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (&seed)[N], const uint32_t (&ctr_hi)[N],
-                         AesCtrGroup* const (&g)[N], uint32_t* l1 = nullptr) {
+                         AesCtrGroup* const (&g)[N]) {
     static_assert(N == 1 || N == 2, "N = 1 or 2");
     const uint4 k0 = rk(0), k1 = rk(1), k2 = rk(2);
     uint32_t L[16 * N];  // 15 used per group
@@ -474,13 +440,9 @@ MH_D void ctr_group_init(const AesPerm& T, const RK& rk, const uint32_t* const (
         l[12] = lds_read_asm(T.a1<1>(a0));
         l[13] = lds_read_asm(T.a2<2>(a1));
         l[14] = lds_read_asm(T.a3<3>(a2));
-        l[15] = l1 ? lds_read_asm(T.a0<0>(a2)) : 0u;
+        l[15] = 0u;
     }
     aes_pin<N>(L);
-    if (l1) {
-#pragma unroll
-        for (int j = 0; j < N; j++) l1[j] = L[16 * j + 15];
-    }
     uint32_t t[N][4];
 #pragma unroll
     for (int j = 0; j < N; j++) {
@@ -576,54 +538,6 @@ MH_D void ctr_blocks_n(const AesPerm& T, const RK& rk, const AesCtrGroup* const 
         out[j][2] = xor3_u32(x[j][2], sd[2] ^ sd[0], ctr[j]);
         out[j][3] = xor3_u32(x[j][3], sd[3], sd[1]);
     }
-}
-
-// ctr_blocks_n<2> with round 1's varying lookup already done (l1, from the
-// previous call's prefetch or ctr_round1) and the NEXT pair's round-1 lookups
-// (LDS addresses pa) issued with this pair's round-3 lookups (results in
-// l1_next): a block pair then costs 9 LDS round trips instead of 10.  In a
-// payload stream the next counter's round-1 address depends only on the
-// counter, so it is known a whole pair ahead.
-template <class RK>
-MH_D void ctr_blocks_pf(const AesPerm& T, const RK& rk, const AesCtrGroup* const (&g)[2],
-                        const uint32_t* const (&seed)[2], const uint32_t (&ctr)[2], const uint32_t (&l1)[2],
-                        const uint32_t (&pa)[2], uint32_t (&l1_next)[2], uint32_t* const (&out)[2]) {
-    uint32_t L2[8];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t u2 = g[j]->p2 ^ l1[j];
-        L2[4 * j + 0] = lds_read_asm(T.a2<2>(u2));
-        L2[4 * j + 1] = lds_read_asm(T.a1<1>(u2));
-        L2[4 * j + 2] = lds_read_asm(T.a0<0>(u2));
-        L2[4 * j + 3] = lds_read_asm(T.a3<3>(u2));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(L2[0]), "+v"(L2[1]), "+v"(L2[2]), "+v"(L2[3]), "+v"(L2[4]), "+v"(L2[5]), "+v"(L2[6]),
-                   "+v"(L2[7]));
-    uint32_t x[2][4];
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) x[j][c] = g[j]->q[c] ^ L2[4 * j + c];
-    aes_round_n_x<2, 2>(T, x, rk(3), pa, l1_next);
-#pragma unroll
-    for (int r = 4; r < 10; r++) aes_round_n<2>(T, x, rk(r));
-    aes_last_n<2>(T, x, rk(10));
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t* sd = seed[j];
-        out[j][0] = x[j][0] ^ sd[2];
-        out[j][1] = x[j][1] ^ sd[3];
-        out[j][2] = xor3_u32(x[j][2], sd[2] ^ sd[0], ctr[j]);
-        out[j][3] = xor3_u32(x[j][3], sd[3], sd[1]);
-    }
-}
-
-// Round 1's varying lookup of two blocks (ctr_blocks_pf's l1), with its own wait.
-MH_D void ctr_round1(const AesCtrGroup* const (&g)[2], const uint32_t (&ctr)[2], uint32_t (&l1)[2]) {
-#pragma unroll
-    for (int j = 0; j < 2; j++) l1[j] = lds_read_asm(g[j]->a ^ ((ctr[j] & 0xffu) << 8));
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(l1[0]), "+v"(l1[1]));
 }
 
 // XofFixedKeyAes128 blocks (seed[j], ctr[j]) for j < N, in lockstep.

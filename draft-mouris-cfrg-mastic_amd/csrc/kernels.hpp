@@ -658,11 +658,6 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
 #ifndef MASTIC_CTR_GROUPS
 #define MASTIC_CTR_GROUPS 1
 #endif
-// the payload loop looks up the next block pair's round-1 byte with this
-// pair's round 3 (aes.hpp ctr_blocks_pf): 9 LDS round trips per pair, not 10
-#ifndef MASTIC_PREFETCH_R1
-#define MASTIC_PREFETCH_R1 0
-#endif
 #define EVAL_PROOF_WAVES 8  // default split (mastic_ctx::proof_waves); measured best of 2..12
 // VGPR cap of the level kernel: 4 waves x 96 per SIMD leave 128 of the 512
 // for one binder-sponge wave (k_absorb_pair), so the two kernels can share a
@@ -858,42 +853,18 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         AesCtrGroup g0, g1;
         uint32_t g_hi = 0;  // counter bits above 7 of the groups (uniform)
         const uint32_t* const csd[2] = {cs0, cs1};
-#if MASTIC_PREFETCH_R1
-        // round 1's varying lookup of the next block pair (ctr_blocks_pf): a
-        // group init returns it for its first counter, every pair prefetches
-        // it for the following one
-        bool have_l1 = false;
-        uint32_t l1[2] = {0u, 0u};
-        auto init_groups = [&](uint32_t hi) {
-            const uint32_t ch2[2] = {hi, hi};
-            AesCtrGroup* const gi[2] = {&g0, &g1};
-            ctr_group_init<2>(TL, rkc, csd, ch2, gi, l1);
-            g_hi = hi;
-            have_l1 = true;
-        };
-#else
         auto init_groups = [&](uint32_t hi) {
             const uint32_t ch2[2] = {hi, hi};
             AesCtrGroup* const gi[2] = {&g0, &g1};
             ctr_group_init<2>(TL, rkc, csd, ch2, gi);
             g_hi = hi;
         };
-#endif
         const AesCtrGroup* const gg[2] = {&g0, &g1};
         init_groups(0u);
         {
             const uint32_t cv[2] = {0u, 0u};
             uint32_t* const ov[2] = {ns0, ns1};
-#if MASTIC_PREFETCH_R1
-            // the next seed (counter 0) prefetches payload block 0's (counter 1)
-            const uint32_t pa[2] = {g0.a ^ (1u << 8), g1.a ^ (1u << 8)};
-            uint32_t l1n[2];
-            ctr_blocks_pf(TL, rkc, gg, csd, cv, l1, pa, l1n, ov);
-            l1[0] = l1n[0];
-            l1[1] = l1n[1];
-#else
             ctr_blocks_n<2>(TL, rkc, gg, csd, cv, ov);
-#endif
         }
 #else
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
@@ -1012,24 +983,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                     wpb = load_wp(e1);
                 }
                 uint32_t o0[4], o1[4];
-#if MASTIC_CTR_GROUPS && MASTIC_PREFETCH_R1
-                {
-                    // round 1 of this pair was looked up with the previous
-                    // pair's round 3 (ctr_blocks_pf), unless a group starts here
-                    const uint32_t c = (uint32_t)(b + 1);
-                    if ((c & ~0xffu) != g_hi) init_groups(c & ~0xffu);  // also looks up round 1 of c
-                    const uint32_t cv[2] = {c, c};
-                    if (!have_l1) ctr_round1(gg, cv, l1);
-                    const uint32_t cn = (c + 1) & 0xffu;  // the next pair's counter, low byte
-                    const uint32_t pa[2] = {g0.a ^ (cn << 8), g1.a ^ (cn << 8)};
-                    uint32_t l1n[2];
-                    uint32_t* const ov[2] = {o0, o1};
-                    ctr_blocks_pf(TL, rkc, gg, csd, cv, l1, pa, l1n, ov);
-                    l1[0] = l1n[0];
-                    l1[1] = l1n[1];
-                    have_l1 = cn != 0;  // 0: the next pair starts a new group
-                }
-#elif MASTIC_CTR_GROUPS
+#if MASTIC_CTR_GROUPS
                 {
                     const uint32_t c = (uint32_t)(b + 1);
                     if ((c & ~0xffu) != g_hi) init_groups(c & ~0xffu);
