@@ -23,8 +23,12 @@ def _current_stream_handle():
 
 
 def gather_shares(local, dist):
-    """All-gather one uint8 tensor per rank into a rank-ordered flat tensor."""
+    """All-gather one uint8 tensor per rank into a rank-ordered flat tensor
+    (RCCL over xGMI for device tensors under the "nccl" backend; a "gloo"
+    group, e.g. several ranks sharing one GPU in a test, gathers host copies)."""
     import torch
+    if local.is_cuda and dist.get_backend() == "gloo":
+        return gather_shares(local.cpu(), dist).to(local.device)
     world = dist.get_world_size()
     out = torch.empty(world * local.numel(), dtype=torch.uint8, device=local.device)
     dist.all_gather_into_tensor(out, local.contiguous())
