@@ -105,6 +105,8 @@ def parse():
     ap.add_argument("--north-star", type=int, default=1,
                     help="c2: after the headline, the north_star job (1M-report full 32-level c2sweep, split over "
                          "the ranks) under a north_star key; 0 skips it")
+    ap.add_argument("--north-star-reports", type=int, default=0,
+                    help="job size of the north_star leg (0 = the 1M of BASELINE.json; smaller only for rehearsals)")
     return ap.parse_args()
 
 
@@ -193,6 +195,17 @@ def cpu_baseline(jobs, procs):
             res = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t
     return wall, res
+
+
+def max_over_ranks(dist, torch, x):
+    """The MAX over ranks of a host float (the timed regions): a device
+    tensor through RCCL, a host one through a gloo rehearsal group."""
+    if dist is None:
+        return x
+    on_gpu = dist.get_backend() != "gloo"
+    tt = torch.tensor([x], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
 
 
 # ---------------------------------------------------------------- sweeps
@@ -402,10 +415,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     dt_local = dt
     (free_b, total_b) = torch.cuda.mem_get_info()
     hbm_used = (total_b - free_b) / 1e9  # whole device, arena and frontier cache included
-    if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(dist, torch, dt)
 
     # units: reports x candidates of both aggregators at every level, over the job
     # (the ranks' shares sum to the job; a virtual rank reports its own share)
@@ -535,10 +545,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         if dist:
             dist.barrier()
         t_spec = time.perf_counter() - t2
-        if dist:
-            tt = torch.tensor([t_spec], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t_spec = float(tt.item())
+        t_spec = max_over_ranks(dist, torch, t_spec)
         out["rates"]["spec_literal_sampled"] = su * world / t_spec
         out["rates"]["spec_literal_sample"] = "%d reports per rank, %d of the sweep's levels (every %d-th), its " \
             "candidate lists, frontier cache off: each level evaluates its whole tree" % (
@@ -670,8 +677,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # MASTIC_BENCH_BACKEND=gloo / MASTIC_BENCH_DEVICE=0: a rehearsal of the
+        # N-rank run with every rank on one GPU (tests); the driver's run is RCCL
+        backend = os.environ.get("MASTIC_BENCH_BACKEND", "nccl")
+        local = int(os.environ.get("MASTIC_BENCH_DEVICE", local))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from mastic_amd import Mastic
     from mastic_amd.merge import aggregate_to_tensor, fold_on_gpu, merge_agg_shares
 
@@ -741,10 +755,7 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(dist, torch, dt)
 
     units = n_rep * len(attrs) * args.steps * world
     value = units / dt
@@ -861,10 +872,7 @@ def main():
         if dist:
             dist.barrier()
         wall = time.perf_counter() - t1
-        if dist:
-            tt = torch.tensor([wall], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            wall = float(tt.item())
+        wall = max_over_ranks(dist, torch, wall)
         out["full_job"] = {
             "reports_per_rank": n_total,
             "job_reports": n_job,
@@ -926,7 +934,7 @@ def main():
         ns_cfg = CONFIGS["c2sweep"]
         try:
             ns = run_sweep(args, ns_cfg, world, rank, local, dist, torch, split=True, steps=1, warmup=1,
-                           n_job=ns_cfg["reports"], emit=False)
+                           n_job=args.north_star_reports or ns_cfg["reports"], emit=False)
         except Exception as e:  # keep the headline line; report the failed leg in it
             import traceback
             traceback.print_exc()
