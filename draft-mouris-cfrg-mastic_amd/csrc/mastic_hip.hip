@@ -649,41 +649,34 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     auto pay_buf = [&](int lv) -> uint32_t* { return plane(wl.payload[lv % NSLOT]); };
     auto oh_gs = [&](int) -> int { return oh_gstride; };
     auto pay_gs = [&](int) -> int { return pay_gstride; };
-    // parts: 1 = the one-hot sponge (level lv's proofs), 2 = the payload
-    // sponge (level lv's parents' payload differences), 3 = both; on stream
-    // `st` (ss unless given), after `ready`.  e4 / e5 (timing) may be null.
-    auto absorb_part = [&](int lv, int parts, hipStream_t st, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
+    auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
         AbsorbArgs ab;
         ab.seg[0] = oh_buf(lv);
         ab.gstride[0] = oh_gs(lv);
-        ab.nbytes[0] = (parts & 1) ? 2 * t->n_parents[lv] * 32 : 0;
+        ab.nbytes[0] = 2 * t->n_parents[lv] * 32;
         ab.f[0] = f_oh;
         ab.seg[1] = pay_buf(lv);
         ab.gstride[1] = pay_gs(lv);
         ab.rstride = bin_rstride;
-        ab.nbytes[1] = (parts & 2) && lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
+        ab.nbytes[1] = lv > 0 ? t->n_parents[lv] * wlw * 4 : 0;
         ab.f[1] = f_pl;
         ab.prio = c->absorb_prio;
         ab.dbg = c->absorb_dbg;
-        HIPCHK(c, hipStreamWaitEvent(st, ready, 0));
-        if (e4) HIPCHK(c, hipEventRecord(e4, st));
+        HIPCHK(c, hipStreamWaitEvent(ss, ready, 0));
+        HIPCHK(c, hipEventRecord(e4, ss));
         if (c->dbg_skip & 4) {
             // timing experiments only: no binder sponges (results wrong)
         } else if (c->absorb_pair)
             hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, 2),
-                               dim3(c->absorb_threads), c->absorb_lds, st, pl, ab);
+                               dim3(c->absorb_threads), c->absorb_lds, ss, pl, ab);
         else
-            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, st, pl, ab);
-        if (e5) HIPCHK(c, hipEventRecord(e5, st));
+            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, ss, pl, ab);
+        HIPCHK(c, hipEventRecord(e5, ss));
         HIPCHK(c, hipGetLastError());
-        f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
-        f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
-        return 0;
-    };
-    auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5) -> int {
-        if (absorb_part(lv, 3, ss, ready, e4, e5)) return -1;
         abs_done[lv] = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(abs_done[lv], ss));
+        f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
+        f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
         return 0;
     };
     // cache planes <-> work planes of this chunk (columns base .. base + n)
@@ -717,7 +710,6 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // parents) instead of a k_node_proof launch: cache hits, and with
     // MASTIC_FUSE_PROOFS=2 cache-on misses too (whole parents only)
     const bool fuse_last = hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs >= 2);
-    hipEvent_t last_aes_done = nullptr;
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
         if (!hit && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
@@ -797,7 +789,6 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipEventRecord(e3, c->stream));
         hipEvent_t aes_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(aes_done, c->stream));
-        last_aes_done = aes_done;
         if (l > 0 && !hit) {
             if (launch_absorb(l - 1, aes_done, e4, e5)) return -1;
         } else {
@@ -837,15 +828,6 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         hipEvent_t e0 = get_event(c, evi++), e1 = get_event(c, evi++);
         hipEvent_t e2 = get_event(c, evi++), e3 = get_event(c, evi++);
         hipEvent_t e4 = get_event(c, evi++), e5 = get_event(c, evi++);
-        // The payload sponge's last segment (the last level's parents' payload
-        // differences, written by the last level kernel) does not need the
-        // last level's proofs: it starts beside k_node_proof, and the one-hot
-        // sponge's last segment follows the proofs on the third stream, so
-        // the serial tail after the last launch is max(payload chain, proofs
-        // + one-hot chain) instead of their sum.  (Pipelined chunks use the
-        // third stream for their odd chunks: they keep the joint launch.)
-        const bool split_tail = !hit && l > 0 && ss == c->stream2 && tail == c->stream && last_aes_done;
-        if (split_tail && absorb_part(l, 2, ss, last_aes_done, e4, nullptr)) return -1;
         HIPCHK(c, hipEventRecord(e0, c->stream));
         HIPCHK(c, hipEventRecord(e1, c->stream));
         HIPCHK(c, hipEventRecord(e2, c->stream));
@@ -855,19 +837,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipGetLastError());
         hipEvent_t np_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(np_done, c->stream));
-        if (split_tail) {
-            // the one-hot chain: after its previous segment (abs_done[l - 1], on ss) and the proofs
-            HIPCHK(c, hipStreamWaitEvent(c->stream3, abs_done[l - 1], 0));
-            if (absorb_part(l, 1, c->stream3, np_done, nullptr, nullptr)) return -1;
-            hipEvent_t oh_done = get_sync_event(c, sev++);
-            HIPCHK(c, hipEventRecord(oh_done, c->stream3));
-            HIPCHK(c, hipStreamWaitEvent(ss, oh_done, 0));
-            HIPCHK(c, hipEventRecord(e5, ss));
-            abs_done[l] = get_sync_event(c, sev++);
-            HIPCHK(c, hipEventRecord(abs_done[l], ss));
-        } else if (launch_absorb(l, np_done, e4, e5)) {
-            return -1;
-        }
+        if (launch_absorb(l, np_done, e4, e5)) return -1;
     }
     if (tail != ss) HIPCHK(c, hipStreamWaitEvent(tail, abs_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
