@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0
 # sweep; it is a parity case, tests/test_gpu_configs.py).  Each entry: Mastic
 # constructor, level, candidate prefixes, default reports per rank per step.
 CONFIGS = {
-    "c2": dict(circuit="Sum", kw=dict(bits=32, max_measurement=255), prefixes=10000, reports=12288,
+    "c2": dict(circuit="Sum", kw=dict(bits=32, max_measurement=255), prefixes=10000, reports=16384,
                total=1000000, full_job=True,
                desc="C2: Mastic(BITS=32, Sum max=255) prep_init+aggregate, level 31"),
     "c3": dict(circuit="Count", kw=dict(bits=256), prefixes=128, reports=16384,
