@@ -824,11 +824,20 @@ def main():
     # when they were measured at this exact workload
     traffic_file = os.path.join(ROOT, "profiles", "eval_traffic.json")
     if os.path.exists(traffic_file):
-        for tr in json.load(open(traffic_file)).get("entries", []):
-            if tr["config"] == args.config and tr["prefixes"] == len(attrs) and tr["reports"] == n_rep:
-                out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
-                out["roofline"]["traffic_unit"] = "bytes per launch"
-                out["roofline"]["traffic_per_step"] = tr["hbm_read_bytes_per_step"] + tr["hbm_write_bytes_per_step"]
+        same = [tr for tr in json.load(open(traffic_file)).get("entries", [])
+                if tr["config"] == args.config and tr["prefixes"] == len(attrs)]
+        exact = [tr for tr in same if tr["reports"] == n_rep]
+        if exact or same:
+            # the level kernel moves a fixed number of bytes per report-node, so a PMC pass at another
+            # batch size scales linearly; the line says which one it is
+            tr = exact[0] if exact else same[0]
+            scale = n_rep / tr["reports"]
+            out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"] * scale
+            out["roofline"]["traffic_unit"] = "bytes per launch"
+            out["roofline"]["traffic_per_step"] = (tr["hbm_read_bytes_per_step"] + tr["hbm_write_bytes_per_step"]) * scale
+            out["roofline"]["traffic_source"] = (
+                "PMC FETCH_SIZE/WRITE_SIZE at this batch size" if exact else
+                "PMC FETCH_SIZE/WRITE_SIZE at %d reports per step, scaled by reports" % tr["reports"])
     # HBM bytes per step, two references (DESIGN.md §4 "HBM traffic"): SURVEY §8d's
     # algorithmic bytes (inputs and outputs only: correction words, input share,
     # prep share) and the floor of the level-synchronous schedule, whose level
