@@ -105,6 +105,12 @@ def parse():
     ap.add_argument("--north-star", type=int, default=1,
                     help="c2: after the headline, the north_star job (1M-report full 32-level c2sweep, split over "
                          "the ranks) under a north_star key; 0 skips it")
+    ap.add_argument("--memory-budget-gb", type=float, default=0,
+                    help="HBM budget per context (0 = the library default, 75%% of free HBM); rehearsals with "
+                         "several ranks sharing one GPU give each rank a slice")
+    ap.add_argument("--lib", default="",
+                    help="A/B tools only: bind this build of libmastic_hip (e.g. an experiment-knobs build) "
+                         "instead of the shipped one; the JSON line then names it under 'library'")
     ap.add_argument("--north-star-reports", type=int, default=0,
                     help="job size of the north_star leg (0 = the 1M of BASELINE.json; smaller only for rehearsals)")
     return ap.parse_args()
@@ -299,10 +305,14 @@ class VirtualRanksMerge:
         enc = m.field.ENCODED_SIZE
         if n_elems == 0:
             return b""
-        local = torch.empty(2 * n_elems * enc, dtype=torch.uint8, device="cuda")
-        for agg_id in range(2):
-            aggregate_to_tensor(m, agg_id, n_elems, valid, out=local[agg_id * n_elems * enc:])
-        merged = np.frombuffer(fold_on_gpu(m, local, 2, n_elems).cpu().numpy().tobytes(), dtype="<u8")
+        if have_results:
+            local = torch.empty(2 * n_elems * enc, dtype=torch.uint8, device="cuda")
+            for agg_id in range(2):
+                aggregate_to_tensor(m, agg_id, n_elems, valid, out=local[agg_id * n_elems * enc:])
+            merged = np.frombuffer(fold_on_gpu(m, local, 2, n_elems).cpu().numpy().tobytes(), dtype="<u8")
+        else:
+            # this rank's share has no reports left (as SweepMerge: zero shares)
+            merged = np.zeros(n_elems, dtype="<u8")
         key = (self.cur[0], tuple(self.cur[1]))
         rest = self.rest.get(key)
         if rest is None:
@@ -338,6 +348,9 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     bits = kw.pop("bits")
     if m is None:
         m = Mastic(bits, cfg["circuit"], device=local, **kw)
+    budget_gb = args.memory_budget_gb or cfg.get("memory_budget_gb")
+    if budget_gb:
+        m.set_memory_budget(int(budget_gb * 2 ** 30))
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(cfg.get("seed_digit", args.config[1]))
     vr = getattr(args, "virtual_ranks", 1) or 1
@@ -376,10 +389,6 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         merge = VirtualRanksMerge(m, alphas_job[n_rep:], w_job[n_rep:])
     else:
         merge = merge_field_shares(m, dist) if dist else None
-    if cfg.get("memory_budget_gb"):
-        import ctypes
-        from mastic_amd import _lib
-        _lib.lib().mastic_set_memory_budget(m._ctx, ctypes.c_uint64(int(cfg["memory_budget_gb"] * 2 ** 30)))
 
     cached_levels = []
     phases = {}
@@ -594,6 +603,8 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         out["cpu_parity"] = parity
     del reps
     if rank == 0 and emit:
+        if args.lib:
+            out["library"] = "alternate build (A/B only): " + args.lib
         print(json.dumps(out))
     if dist and emit:
         dist.destroy_process_group()
@@ -686,6 +697,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    if args.lib:
+        from mastic_amd import _lib
+        _lib.load(args.lib)
     from mastic_amd import Mastic
     from mastic_amd.merge import aggregate_to_tensor, fold_on_gpu, merge_agg_shares
 
@@ -702,10 +716,17 @@ def main():
         # (the full_job leg is then strong scaling)
         n_job = n_total
         (lo, hi) = split_bounds(n_job, world)[rank]
-        n_total = max(n_rep, hi - lo)
+        if hi - lo < 1:
+            raise SystemExit("--split: %d resident reports leave rank %d none" % (n_job, rank))
+        # a rank's steps run within its own share of the job, so value (job
+        # reports x prefixes / wall) counts exactly the reports processed
+        n_rep = min(n_rep, hi - lo)
+        n_total = hi - lo
     kw = dict(cfg["kw"])
     bits = kw.pop("bits")
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
+    if args.memory_budget_gb:
+        m.set_memory_budget(int(args.memory_budget_gb * 2 ** 30))
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
     # distinct reports resident in HBM: all of them, or a pool the job cycles through
@@ -830,7 +851,7 @@ def main():
         if exact or same:
             # the level kernel moves a fixed number of bytes per report-node, so a PMC pass at another
             # batch size scales linearly; the line says which one it is
-            tr = exact[0] if exact else same[0]
+            tr = exact[0] if exact else min(same, key=lambda e: abs(e["reports"] - n_rep))
             scale = n_rep / tr["reports"]
             out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"] * scale
             out["roofline"]["traffic_unit"] = "bytes per launch"
@@ -977,9 +998,18 @@ def main():
             out["north_star"]["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind",
                                                                     "single_process_value", "sample")}
             out["north_star"]["cpu_parity"] = ns.get("cpu_parity")
-            out["north_star"]["speedup_vs_cpu_pool"] = ns["value"] / cb["value"]
-            out["north_star"]["speedup_vs_cpu_core"] = ns["value"] / cb["single_process_value"]
+            # like for like: the CPU leg evaluates whole trees (spec-literal, no
+            # cache), so the spec-literal GPU rate is the comparable one; the
+            # cached rate's ratio is kept beside it, labelled
+            lit = ns["rates"].get("spec_literal_sampled")
+            if lit:
+                out["north_star"]["speedup_spec_literal_vs_cpu_pool"] = lit / cb["value"]
+                out["north_star"]["speedup_spec_literal_vs_cpu_core"] = lit / cb["single_process_value"]
+            out["north_star"]["speedup_cached_vs_cpu_pool"] = ns["value"] / cb["value"]
+            out["north_star"]["speedup_cached_vs_cpu_core"] = ns["value"] / cb["single_process_value"]
     if rank == 0:
+        if args.lib:
+            out["library"] = "alternate build (A/B only): " + args.lib
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -189,7 +189,21 @@ struct mastic_ctx {
     int absorb_threads = 256;            // threads per binder-sponge workgroup (MASTIC_ABSORB_THREADS)
     int absorb_prio = 3;                 // s_setprio of the binder sponge waves (MASTIC_ABSORB_PRIO)
     int absorb_dbg = 0;                  // timing experiments only (MASTIC_ABSORB_DBG, kernels.hpp AbsorbArgs::dbg)
-    int force_slow_blk = -1;    // test hook (MASTIC_FORCE_SLOW_BLK): exact payload stream from this block on
+    // result-preserving test hooks (mastic_set_test_hooks; nothing in the environment sets them)
+    int force_slow_blk = -1;    // exact payload stream from this block on
+    int fail_allocs = 0;        // this many result / cache-slot allocations fail first (ENOMEM recovery)
+    bool inject_alloc_failure() {
+        if (fail_allocs <= 0) return false;
+        fail_allocs--;
+        return true;
+    }
+    // Wait for everything queued on the ctx's three streams (explicitly: the
+    // recovery paths below free buffers that queued kernels on any of them may
+    // still read, so they must not rely on hipFree's implicit device wait).
+    bool idle() {
+        return hipStreamSynchronize(stream) == hipSuccess && hipStreamSynchronize(stream2) == hipSuccess &&
+               hipStreamSynchronize(stream3) == hipSuccess;
+    }
     bool fc_all = false;        // A/B only: the frontier-cache kernel variant at every level (MASTIC_FC_ALL=1)
     int fuse_proofs = 1;        // last level's node proofs in the level kernel: 1 on cache hits, 2 also on
                                 // cache-on misses, 0 never (MASTIC_FUSE_PROOFS; else k_node_proof)
@@ -923,12 +937,13 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         d.p = nullptr;
         d.bytes = 0;
         d.own = true;
-        if (d.ensure(std::max(want, old + old / 2)) || d.ensure(want)) return true;
+        if (!c->inject_alloc_failure() && (d.ensure(std::max(want, old + old / 2)) || d.ensure(want))) return true;
         // HBM is held by the work arena (sized to the budget when the results
-        // were smaller) and by retired buffers: once the queued work is done,
-        // free both and retry; the arena is re-allocated below, within what is
-        // left (a 2M-report sweep's out shares reach 32 GB per aggregator)
-        if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+        // were smaller) and by retired buffers: once the queued work on all
+        // three streams is done, free both and retry; the arena is re-allocated
+        // below, within what is left (a 2M-report sweep's out shares reach 32 GB
+        // per aggregator)
+        if (!c->idle()) return false;
         c->bury();
         c->work.release();
         return d.ensure(want);
@@ -984,8 +999,8 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         // an allocation that fails first reclaims what idle streams free: the
         // retired slots and the work buffer (re-allocated below, to the budget)
         auto alloc = [&](DevBuf& b, size_t bytes) -> bool {
-            if (b.ensure(bytes)) return true;
-            if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+            if (!c->inject_alloc_failure() && b.ensure(bytes)) return true;
+            if (!c->idle()) return false;
             c->bury();
             c->work.release();
             return b.ensure(bytes);
@@ -1005,7 +1020,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
             }
             DevBuf ncs, ncv;
             if (!c->graveyard.empty()) {  // the other aggregator's retired slot: free it first
-                if (hipStreamSynchronize(c->stream) == hipSuccess) c->bury();
+                if (c->idle()) c->bury();
             }
             ok = alloc(ncs, cap * 5 * S1 * 4) && alloc(ncv, cap * 4 * S1 * 4);
             if (ok) {
@@ -1070,7 +1085,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         const size_t arena = std::max(want, std::min<size_t>(lc ? c->work_arena_fc : c->work_arena, budget));
         if (!c->work.ensure(arena) && !c->work.ensure(want)) {
             // retired buffers (cache slots, evicted trees) are freed once the stream is idle
-            if (c->graveyard.empty() || hipStreamSynchronize(c->stream) != hipSuccess)
+            if (c->graveyard.empty() || !c->idle())
                 return fail(c, MASTIC_ENOMEM, "out of device memory (work %zu bytes)", want);
             c->bury();
             if (!c->work.ensure(arena) && !c->work.ensure(want))
@@ -1322,8 +1337,8 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     return 0;
 }
 
-extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share,
-                                       void* caller_stream) {
+extern "C" int mastic_aggregate_device_on_stream(mastic_ctx* c, int agg_id, const uint8_t* valid,
+                                                 void* dev_agg_share, void* caller_stream) {
     DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     Result& R = c->res[agg_id];
@@ -1340,6 +1355,11 @@ extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t*
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's stream (e.g. RCCL's) reads it next
     return 0;
+}
+
+// The round-2 signature (ABI version 3): ordered after the null stream's work.
+extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share) {
+    return mastic_aggregate_device_on_stream(c, agg_id, valid, dev_agg_share, nullptr);
 }
 
 extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t n_shares, size_t n_elems,
@@ -1733,14 +1753,6 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->p = p;
     c->device = up->device;
     c->n_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    // Test hook (MASTIC_FORCE_SLOW_BLK, result-preserving): the payload fast
-    // path hands over to the exact rejection-sampling stream at this block, so
-    // the tests reach the handover that random data hits with probability
-    // 2^-32 per candidate.  Outputs are identical either way.
-    {
-        const char* fs = getenv("MASTIC_FORCE_SLOW_BLK");
-        c->force_slow_blk = fs ? atoi(fs) : -1;
-    }
 #ifdef MASTIC_EXPERIMENT_KNOBS
     // A/B and timing experiments only (tools/ab_*.sh build the library with
     // -DMASTIC_EXPERIMENT_KNOBS; the shipped library reads none of these).
@@ -1847,6 +1859,16 @@ extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
     if (last_hit) *last_hit = c->last_hit ? 1 : 0;
     return 0;
 }
+
+extern "C" int mastic_set_test_hooks(mastic_ctx* c, int force_slow_blk, int fail_allocs) {
+    if (!c) return MASTIC_EINVAL;
+    const int pending = c->fail_allocs;
+    c->force_slow_blk = force_slow_blk < 0 ? -1 : force_slow_blk;
+    c->fail_allocs = std::max(0, fail_allocs);
+    return pending;
+}
+
+extern "C" int mastic_abi_version(void) { return MASTIC_ABI_VERSION; }
 
 extern "C" int mastic_set_memory_budget(mastic_ctx* c, uint64_t bytes) {
     if (!c) return MASTIC_EINVAL;

@@ -15,8 +15,10 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(PKG_DIR, "libmastic_hip.so")
-# experiments only: load another build of the same library
-LOAD_PATH = os.environ.get("MASTIC_LIB", LIB_PATH)
+# The library lib() loads: always the shipped in-tree build, unless an A/B tool
+# calls load(path) explicitly (no process variable can swap it).
+LOAD_PATH = LIB_PATH
+ABI_VERSION = 4  # include/mastic_hip.h MASTIC_ABI_VERSION
 
 MASTIC_OK = 0
 ERRORS = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -5: "EHIP"}
@@ -31,6 +33,7 @@ EXPORTS = [
     "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
     "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
     "mastic_aggregate_device", "mastic_reports_view", "mastic_decide_results",
+    "mastic_aggregate_device_on_stream", "mastic_abi_version", "mastic_set_test_hooks",
 ]
 
 
@@ -65,8 +68,8 @@ class MasticError(RuntimeError):
 def build(verbose=False, force=False, out=None, defines=()) -> str:
     """Compile csrc/mastic_hip.hip for gfx950 into the package directory.
     ``out`` / ``defines``: another build of the same source (e.g.
-    ``defines=("MASTIC_EXPERIMENT_KNOBS",)`` for the A/B tools, loaded through
-    MASTIC_LIB); the shipped library is the default one."""
+    ``defines=("MASTIC_EXPERIMENT_KNOBS",)`` for the A/B tools, which load it
+    through ``load(path)``); the shipped library is the default one."""
     out = out or LIB_PATH
     srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
     srcs.append(os.path.join(INCLUDE, "mastic_hip.h"))
@@ -86,6 +89,17 @@ def build(verbose=False, force=False, out=None, defines=()) -> str:
 
 _lib = None
 _lock = threading.Lock()
+
+
+def load(path: str):
+    """A/B and timing tools only: bind another build of the library (e.g. a
+    -DMASTIC_EXPERIMENT_KNOBS build) instead of the shipped one.  Must be
+    called before the first lib() call of the process."""
+    global LOAD_PATH
+    with _lock:
+        if _lib is not None and os.path.abspath(path) != os.path.abspath(LOAD_PATH):
+            raise RuntimeError("libmastic_hip is already loaded from %s" % LOAD_PATH)
+        LOAD_PATH = os.path.abspath(path)
 
 
 def lib():
@@ -124,7 +138,10 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
                     "mastic_fold_shares": (i32, [P, P, sz, sz, P, P]),
-                    "mastic_aggregate_device": (i32, [P, i32, P, P, P]),
+                    "mastic_aggregate_device": (i32, [P, i32, P, P]),
+                    "mastic_aggregate_device_on_stream": (i32, [P, i32, P, P, P]),
+                    "mastic_abi_version": (i32, []),
+                    "mastic_set_test_hooks": (i32, [P, i32, i32]),
                     "mastic_reports_view": (i32, [P, sz, sz, ctypes.POINTER(P)]),
                     "mastic_decide_results": (i32, [P, u8p, sz, P, P]),
                     "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3
@@ -139,6 +156,9 @@ def lib():
                     fn = getattr(l, name)
                     fn.restype = res
                     fn.argtypes = args
+                if l.mastic_abi_version() != ABI_VERSION:
+                    raise ImportError("%s has ABI version %d, this binding expects %d (rebuild it)"
+                                      % (LOAD_PATH, l.mastic_abi_version(), ABI_VERSION))
                 _lib = l
     return _lib
 

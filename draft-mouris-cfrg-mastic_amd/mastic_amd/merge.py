@@ -58,10 +58,10 @@ def aggregate_to_tensor(m, agg_id, n_elems, valid=None, out=None):
     if out is None:
         out = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device="cuda")
     v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-    rc = _lib.lib().mastic_aggregate_device(m._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(out.data_ptr()),
-                                            _current_stream_handle())
+    rc = _lib.lib().mastic_aggregate_device_on_stream(m._ctx, agg_id, _lib.buf(v),
+                                                      ctypes.c_void_p(out.data_ptr()), _current_stream_handle())
     if rc != 0:
-        raise _lib.MasticError(rc, "mastic_aggregate_device failed")
+        raise _lib.MasticError(rc, "mastic_aggregate_device_on_stream failed")
     return out
 
 

@@ -236,13 +236,13 @@ class Mastic:
         _check(self._ctx, _lib.lib().mastic_prep_result(self._ctx, agg_id, None, None, None, None))
 
     def aggregate_to(self, agg_id: int, valid, dev_ptr: int, stream: int = 0):
-        """``mastic_aggregate_device``: fold into caller-owned device memory
+        """``mastic_aggregate_device_on_stream``: fold into caller-owned device memory
         (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM.
         ``stream`` is the hipStream_t handle whose queued work last touched
         the buffer (0 = the null stream)."""
         v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-        _check(self._ctx, _lib.lib().mastic_aggregate_device(self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr),
-                                                             ctypes.c_void_p(stream or None)))
+        _check(self._ctx, _lib.lib().mastic_aggregate_device_on_stream(
+            self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None)))
 
     def aggregate_device(self, agg_id: int, agg_param, valid=None, raw=False):
         """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU
@@ -318,6 +318,24 @@ class Mastic:
         _check(self._ctx, _lib.lib().mastic_tree_stats(self._ctx, enc, len(enc), ctypes.byref(a),
                                                        ctypes.byref(b), ctypes.byref(c)))
         return (a.value, b.value, c.value)
+
+    def set_memory_budget(self, nbytes: int):
+        """HBM budget for one prep_init's work buffers (``mastic_set_memory_budget``;
+        0 = 75 % of the free HBM).  Several contexts sharing one GPU (ranks of a
+        one-GPU rehearsal) each take a slice."""
+        _check(self._ctx, _lib.lib().mastic_set_memory_budget(self._ctx, ctypes.c_uint64(int(nbytes))))
+
+    def set_test_hooks(self, force_slow_blk: int = -1, fail_allocs: int = 0):
+        """Result-preserving test hooks of this context (``mastic_set_test_hooks``):
+        hand the payload fast path over to the exact next_vec stream at convert
+        block ``force_slow_blk`` (-1: off), and make the next ``fail_allocs``
+        result / cache-slot allocations fail as if HBM were exhausted (the
+        ENOMEM recovery path).  Outputs are identical either way.  Returns how
+        many injected failures the previous setting had not yet used."""
+        rc = _lib.lib().mastic_set_test_hooks(self._ctx, int(force_slow_blk), int(fail_allocs))
+        if rc < 0:
+            _check(self._ctx, rc)
+        return rc
 
     def set_frontier_cache(self, on: bool):
         """Keep each prep_init's per-level binder inputs and last frontier in HBM so

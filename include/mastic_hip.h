@@ -42,6 +42,10 @@
 extern "C" {
 #endif
 
+/* ABI version of this header; mastic_abi_version() returns the library's.
+ * 4: mastic_aggregate_device_on_stream, mastic_set_test_hooks. */
+#define MASTIC_ABI_VERSION 4
+
 #define MASTIC_OK 0
 #define MASTIC_EINVAL (-22)
 #define MASTIC_ENOMEM (-12)
@@ -147,9 +151,11 @@ int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t*
  * leaves HBM.  caller_stream is the hipStream_t whose queued work last
  * touched the buffer (e.g. the stream it was allocated or zero-filled on;
  * NULL = the null stream): the fold is ordered after that work by an event.
- * Returns when the buffer is written. */
-int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
-                            void* caller_stream);
+ * Returns when the buffer is written.  (ABI 4; the ABI-3 form without a
+ * stream, mastic_aggregate_device, orders after the null stream.) */
+int mastic_aggregate_device_on_stream(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
+                                      void* caller_stream);
+int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share);
 /* Multi-GPU merge (Mastic.merge, mastic.py:390-397) of n_shares agg shares
  * of n_elems elements each, all in DEVICE memory of the ctx's GPU (e.g. the
  * output of an RCCL all-gather): dev_out[e] = sum_s dev_shares[s][e] mod p.
@@ -185,6 +191,20 @@ int mastic_proof_tree(mastic_ctx* ctx, int agg_id, const uint8_t* app_ctx, size_
 int mastic_set_frontier_cache(mastic_ctx* ctx, int on, int* last_hit);
 /* Wait for all enqueued work of the ctx. */
 int mastic_synchronize(mastic_ctx* ctx);
+/* The library's MASTIC_ABI_VERSION (a caller built against another header
+ * version must not bind it). */
+int mastic_abi_version(void);
+/* Result-preserving test hooks of one ctx (tests only; the library reads no
+ * environment variable that changes computation).  force_slow_blk >= 0: the
+ * level kernel's speculative payload path hands over to the exact
+ * rejection-sampling stream (vidpf.py:352-364 next_vec) at this convert block,
+ * which random data reaches with probability ~2^-32 per candidate; -1 off.
+ * fail_allocs: the next that many result-buffer / frontier-cache-slot
+ * allocations fail as if HBM were exhausted, driving the recovery path (wait
+ * for the ctx's streams, free retired buffers and the work arena, retry).
+ * Outputs are identical either way.  Returns the number of injected failures
+ * the previous setting still had pending (>= 0), or MASTIC_EINVAL. */
+int mastic_set_test_hooks(mastic_ctx* ctx, int force_slow_blk, int fail_allocs);
 
 /* One-shot host-buffer form of upload + prep_init + prep_result. */
 int mastic_prep_init_batch(mastic_ctx* ctx, const uint8_t* verify_key, size_t verify_key_len,

@@ -67,13 +67,42 @@ def test_shipped_library_reads_no_experiment_knobs():
     MASTIC_ABSORB_DBG) are compiled only into -DMASTIC_EXPERIMENT_KNOBS
     builds: the shipped library does not even contain their names, so a stray
     variable in an aggregator's environment cannot change its results.  The
-    only variable it reads that touches computation is the result-preserving
-    test hook MASTIC_FORCE_SLOW_BLK (exact-stream handover)."""
+    result-preserving test hooks (exact-stream handover, forced allocation
+    failures) are set per ctx through mastic_set_test_hooks, not read from the
+    environment."""
     data = open(_lib_path(), "rb").read()
     for knob in (b"MASTIC_DBG_SKIP", b"MASTIC_ABSORB_DBG", b"MASTIC_ABSORB_SINGLE", b"MASTIC_PROOF_WAVES",
-                 b"MASTIC_BINDER_TILED", b"MASTIC_CHUNK_REPORTS", b"MASTIC_SPLIT_ELEMS", b"MASTIC_FC_ALL"):
+                 b"MASTIC_BINDER_TILED", b"MASTIC_CHUNK_REPORTS", b"MASTIC_SPLIT_ELEMS", b"MASTIC_FC_ALL",
+                 b"MASTIC_FORCE_SLOW_BLK"):
         assert knob not in data, knob
-    assert b"MASTIC_FORCE_SLOW_BLK" in data
+
+
+def test_default_import_cannot_load_another_build(tmp_path):
+    """The product loader binds the shipped in-tree library whatever the
+    environment says (round 3 let MASTIC_LIB swap in a knobs build): only an
+    explicit _lib.load(path) call, which the A/B tools make, selects another
+    build.  Checked in a fresh interpreter with MASTIC_LIB pointing at a file
+    that is not the library."""
+    import subprocess
+    import sys
+    bogus = tmp_path / "libmastic_knobs.so"
+    bogus.write_bytes(b"not a library")
+    env = dict(os.environ, MASTIC_LIB=str(bogus))
+    code = ("import sys; sys.path.insert(0, %r); from mastic_amd import _lib; "
+            "print(_lib.LOAD_PATH == _lib.LIB_PATH)" % os.path.join(ROOT, "draft-mouris-cfrg-mastic_amd"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "True"
+    src = open(os.path.join(ROOT, "draft-mouris-cfrg-mastic_amd", "mastic_amd", "_lib.py")).read()
+    assert "environ" not in src
+
+
+def test_library_abi_version_matches_binding():
+    from mastic_amd import _lib
+    lib = ctypes.CDLL(_lib_path())
+    lib.mastic_abi_version.restype = ctypes.c_int
+    assert lib.mastic_abi_version() == _lib.ABI_VERSION
+    text = open(os.path.join(ROOT, "include", "mastic_hip.h")).read()
+    assert re.search(r"#define MASTIC_ABI_VERSION %d\b" % _lib.ABI_VERSION, text)
 
 
 def test_product_has_no_device_wide_sync():
@@ -84,3 +113,20 @@ def test_product_has_no_device_wide_sync():
     for f in os.listdir(csrc):
         text = re.sub(r"//.*", "", open(os.path.join(csrc, f)).read())
         assert "hipDeviceSynchronize" not in text, f
+
+
+def test_integration_stub_binds_the_library():
+    """integration/poc/mastic_hip.py loads and binds the
+    shipped library on a CPU-only host (no compute call): every entry point
+    it uses exists, mastic_last_error returns text (restype c_char_p) and the
+    ABI versions agree."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "mastic_hip_stub", os.path.join(ROOT, "integration", "poc", "mastic_hip.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    lib = mod.load(_lib_path())
+    assert lib.mastic_last_error.restype is ctypes.c_char_p
+    assert lib.mastic_last_error(None) == b"null ctx"
+    from mastic_amd import _lib
+    assert mod.ABI_VERSION == _lib.ABI_VERSION

@@ -31,3 +31,45 @@ def test_bench_two_ranks_on_one_gpu():
     ns = d["north_star"]
     assert ns["n_gpus"] == 2 and ns["scaling"] == "strong" and ns["job_reports"] == 16384
     assert ns["heavy_hitters_equal_plaintext"] is True
+
+
+def _run_bench(args, timeout=500):
+    env = dict(os.environ, MASTIC_BENCH_BACKEND="gloo", MASTIC_BENCH_DEVICE="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_four_ranks_uneven_job_on_one_gpu():
+    """`--gpus 4` (four ranks through torch.distributed.run, gloo, one GPU,
+    6 GiB of HBM budget per rank): C2 steps with the merge, and the
+    north_star leg over a job of 16,387 reports, which four ranks cannot split
+    evenly (split_bounds: 4,096 / 4,097 / 4,097 / 4,097); the heavy hitters
+    and sampled levels' aggregates equal the plaintext ones."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = _run_bench(["--gpus", "4", "--steps", "1", "--warmup", "1", "--reports", "512", "--total-reports", "512",
+                    "--north-star-reports", "16387", "--cpu-baseline", "0", "--memory-budget-gb", "6"])
+    assert d["n_gpus"] == 4 and d["value"] > 0
+    ns = d["north_star"]
+    assert ns["n_gpus"] == 4 and ns["job_reports"] == 16387
+    assert ns["heavy_hitters"] > 0 and ns["heavy_hitters_equal_plaintext"] is True
+
+
+def test_bench_four_ranks_one_rank_without_reports():
+    """A split sweep job of 3 reports over 4 ranks: rank 0 holds none
+    (split_bounds gives it [0, 0)), so at every level it contributes zero
+    shares through SweepMerge.total(have_results=False) to the same
+    collectives as the other ranks.  The job's heavy hitters (every attribute
+    with weight >= the threshold of 1) and sampled levels' aggregates equal
+    the plaintext ones."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = _run_bench(["--gpus", "4", "--config", "c2sweep", "--split", "1", "--reports", "3", "--steps", "1",
+                    "--warmup", "0", "--cpu-baseline", "0", "--memory-budget-gb", "2"])
+    c = d["config"]
+    assert d["n_gpus"] == 4 and c["job_reports"] == 3 and c["reports_this_rank"] == 0
+    assert c["heavy_hitters_equal_plaintext"] is True

@@ -378,16 +378,16 @@ def test_c2_shape_properties_and_oracle_sample(mastic_amd):
 
 
 @pytest.mark.parametrize("blk", [0, 1, 4, 8])
-def test_fast_path_handover_to_exact_stream(mastic_amd, blk, monkeypatch):
+def test_fast_path_handover_to_exact_stream(mastic_amd, blk):
     """The Field64 level kernel speculates that no next_vec candidate is
     rejected and hands over to the exact rejection-sampling stream when one
     might be (probability 2^-32 per candidate, never hit by random tests).
     Force the handover at block `blk` and check every output against the
     oracle: elements before the handover come from the fast path, the rest
     from the exact stream."""
-    monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
     rng = random.Random(100 + blk)
     m = mastic_amd.MasticSum(6, 255)  # VALUE_LEN 17: 9 payload blocks per node
+    m.set_test_hooks(force_slow_blk=blk)
     o = _oracle_for(m)
     (alphas, weights, nonces, rands) = _random_reports(m, rng, 4)
     vk = bytes(rng.getrandbits(8) for _ in range(32))
@@ -396,12 +396,12 @@ def test_fast_path_handover_to_exact_stream(mastic_amd, blk, monkeypatch):
 
 
 @pytest.mark.parametrize("blk", [0, 2, 6])
-def test_fast_path_handover_field128(mastic_amd, blk, monkeypatch):
+def test_fast_path_handover_field128(mastic_amd, blk):
     """Same handover for the Field128 fast path (one candidate per block; a
     candidate >= p has its top word 0xffffffff)."""
-    monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
     rng = random.Random(200 + blk)
     m = mastic_amd.MasticHistogram(5, 7, 3)  # VALUE_LEN 8: 8 payload blocks per node
+    m.set_test_hooks(force_slow_blk=blk)
     o = _oracle_for(m)
     (alphas, weights, nonces, rands) = _random_reports(m, rng, 4)
     vk = bytes(rng.getrandbits(8) for _ in range(32))
@@ -515,16 +515,15 @@ def test_c2_full_prefix_count_oracle_report(mastic_amd):
 
 
 @pytest.mark.parametrize("blk", [-1, 0, 150, 250])
-def test_field128_long_payload_handover(mastic_amd, blk, monkeypatch):
+def test_field128_long_payload_handover(mastic_amd, blk):
     """A long Field128 payload (VALUE_LEN 301: 301 convert blocks per child,
     the C5 shape at a smaller length).  Every output against the oracle, also
     with the exact-stream handover forced early, in the middle and near the
     end of the payload (the exact stream restarts from element 0 and emits
     from the handover element on)."""
-    if blk >= 0:
-        monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(blk))
     rng = random.Random(400 + blk)
     m = mastic_amd.MasticSumVec(4, 300, 1, 10)
+    m.set_test_hooks(force_slow_blk=blk)
     assert m.VALUE_LEN == 301
     o = _oracle_for(m)
     (alphas, weights, nonces, rands) = _random_reports(m, rng, 3)

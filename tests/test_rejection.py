@@ -107,16 +107,14 @@ def test_gpu_matches_rejection_fixture(name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("force_slow", [None, 0, 3])
 @pytest.mark.parametrize("name", FIXTURES)
-def test_gpu_cache_hit_recomputes_rejected_parent(name, force_slow, monkeypatch):
+def test_gpu_cache_hit_recomputes_rejected_parent(name, force_slow):
     """Frontier-cache hit over the fixture's rejected node: at level 1 both
     level-0 nodes are parents, and the cached call recomputes each parent's
     payload from its cached convert seed -- for report B through the real
-    rejection (the exact next_vec stream), and with MASTIC_FORCE_SLOW_BLK
-    through a forced handover at a payload block.  Prep shares and out shares
+    rejection (the exact next_vec stream), and with the force_slow_blk test
+    hook (mastic_set_test_hooks) through a forced handover at a payload block.  Prep shares and out shares
     of the hit equal a context without the cache and the oracle."""
     import mastic_amd
-    if force_slow is not None:
-        monkeypatch.setenv("MASTIC_FORCE_SLOW_BLK", str(force_slow))
     fx = _load(name)
 
     def mk():
@@ -124,6 +122,9 @@ def test_gpu_cache_hit_recomputes_rejected_parent(name, force_slow, monkeypatch)
             return mastic_amd.MasticSum(fx["bits"], 255)
         return mastic_amd.MasticHistogram(fx["bits"], 64, 8)
     m_on, m_off = mk(), mk()
+    if force_slow is not None:
+        for m in (m_on, m_off):
+            m.set_test_hooks(force_slow_blk=force_slow)
     m_on.set_frontier_cache(True)
     o = _oracle(fx)
     ctx, nonce = bytes.fromhex(fx["ctx"]), bytes.fromhex(fx["nonce"])

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing: GPU tests with the default build, then the C2 bench for the
-# default build, each build/lib*.so variant (MASTIC_LIB override) and each
+# default build, each build/lib*.so variant (bench.py --lib) and each
 # "NAME=ENV=VALUE" entry of $AB_ENVS.
 set -o pipefail
 if [ -z "$AB_NOTEST" ]; then
@@ -11,7 +11,7 @@ for R in ${AB_REPORTS:-8192 4096}; do
   for f in build/lib*.so; do
     [ -e "$f" ] || continue
     v=$(basename $f .so)
-    MASTIC_LIB=$PWD/$f timeout -k 10 200 python bench.py --reports $R --steps 2 --warmup 1 --cpu-baseline 0 > gpurun_out/ab_${v}_$R.json || exit $?
+    timeout -k 10 200 python bench.py --lib $PWD/$f --reports $R --steps 2 --warmup 1 --cpu-baseline 0 > gpurun_out/ab_${v}_$R.json || exit $?
   done
   for e in $AB_ENVS; do
     name=${e%%=*}; kv=${e#*=}

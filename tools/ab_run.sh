@@ -2,7 +2,7 @@
 # A/B timing on one GPU box (run through gpurun from the repo root):
 #   tools/ab_run.sh <tag> <reps> <variant> [<variant> ...]
 # variant = name|ENV=V,ENV=V|config|extra+bench+args   (fields may be empty;
-# MASTIC_LIB=build/lib....so selects another build of the library).
+# LIB=build/lib....so selects another build of the library: bench.py --lib).
 # Variants run interleaved <reps> times (A B A B ...) so box drift hits all
 # alike; each run under its own time limit; a failure ends the script.
 # Output: gpurun_out/<tag>/<name>_<rep>.json (+ .log), summary.txt
@@ -17,12 +17,14 @@ for rep in $(seq 1 "$REPS"); do
         cfg=${cfg:-c2}
         args=${args//+/ }
         envarr=()
-        if [ -n "$envs" ]; then IFS=',' read -r -a envarr <<< "$envs"; fi
-        for i in "${!envarr[@]}"; do
-            case ${envarr[$i]} in MASTIC_LIB=*) envarr[$i]="MASTIC_LIB=$PWD/${envarr[$i]#MASTIC_LIB=}" ;; esac
+        lib=()
+        if [ -n "$envs" ]; then IFS=',' read -r -a ev <<< "$envs"; fi
+        for e in "${ev[@]}"; do
+            case $e in LIB=*) lib=(--lib "$PWD/${e#LIB=}") ;; *) envarr+=("$e") ;; esac
         done
-        echo "[$(date +%T)] $name rep $rep: ${envarr[*]} bench --config $cfg $args" >> "$OUT/steps.txt"
-        env "${envarr[@]}" timeout -k 10 300 python3 -u bench.py --config "$cfg" --cpu-baseline 0 --full-job 0 $args \
+        unset ev
+        echo "[$(date +%T)] $name rep $rep: ${envarr[*]} bench --config $cfg $args ${lib[*]}" >> "$OUT/steps.txt"
+        env "${envarr[@]}" timeout -k 10 300 python3 -u bench.py --config "$cfg" --cpu-baseline 0 --full-job 0 $args "${lib[@]}" \
             > "$OUT/${name}_$rep.log" 2>&1
         rc=$?
         if [ $rc -ne 0 ]; then echo "$name rc=$rc" >> "$OUT/steps.txt"; tail -20 "$OUT/${name}_$rep.log"; exit $rc; fi

@@ -7,8 +7,8 @@ B="python3 bench.py --config c2 --steps 4 --warmup 1 --cpu-baseline 0 --full-job
 NT=$PWD/draft-mouris-cfrg-mastic_amd/mastic_amd/libmastic_hip_nt.so
 for i in 1 2; do
 run base_$i $B
-run nt_$i env MASTIC_LIB=$NT $B
+run nt_$i $B --lib $NT
 done
-run c5_nt env MASTIC_LIB=$NT python3 bench.py --config c5 --steps 3 --warmup 1 --cpu-baseline 0
+run c5_nt python3 bench.py --config c5 --steps 3 --warmup 1 --cpu-baseline 0 --lib $NT
 run c5_base python3 bench.py --config c5 --steps 3 --warmup 1 --cpu-baseline 0
 echo done >> $O/steps.txt

@@ -1,4 +1,4 @@
-"""Replace one config's entry of profiles/eval_traffic.json (the HBM bytes bench.py reports as
+"""Add or replace one (config, prefixes, reports) entry of profiles/eval_traffic.json (the HBM bytes bench.py reports as
 roofline.traffic) with the FETCH_SIZE / WRITE_SIZE passes of a tools/gpu_session.sh pmc:<cfg> run.
 
     python tools/update_eval_traffic.py <pmc_summary.json> <cfg> <reports> <prefixes> <kernel> <tag>
@@ -23,7 +23,9 @@ def main(summary, cfg, reports, prefixes, kernel, tag):
         "hbm_gbs_serialized": (rd + wr) / (s["serial_ms"] / 1e3) / 1e9,
         "measured": "%s (%s)" % (tag, os.path.relpath(summary, ROOT)),
     }
-    d["entries"] = [e for e in d["entries"] if e["config"] != cfg] + [entry]
+    # one entry per (config, prefixes, reports): measurements at other batch sizes stay
+    d["entries"] = [e for e in d["entries"]
+                    if (e["config"], e["prefixes"], e["reports"]) != (cfg, int(prefixes), int(reports))] + [entry]
     json.dump(d, open(path, "w"), indent=1)
     print(json.dumps(entry, indent=1))
 
