@@ -667,7 +667,11 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
 #define EVAL_MIN_WAVES 5
 #endif
 #define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(EVAL_MIN_WAVES)))
-#define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16 + 16)
+// workgroup sync words after the key schedules: [0] parent-run counter, [1]
+// node-proof counter (frontier-cache hits), [8, 40) "child seeds stored" bitmap
+// of the workgroup's parents (<= 16 waves x 64 parents per wave)
+#define EVAL_SYNC_WORDS 40
+#define EVAL_LDS_BYTES (AES_PERM_LDS_WORDS * 4 + 2 * 64 * 11 * 16 + 4 * EVAL_SYNC_WORDS)
 // GEN: the general level (the root level, which writes the root sum instead
 // of parent payload differences, and the last level, which emits the
 // truncated out shares, with their field multiplications for grouped
@@ -689,6 +693,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     uint4* RKE = eval_lds + AES_PERM_LDS_WORDS / 4;
     uint4* RKC = RKE + 64 * 11;
     uint32_t* next_parent = (uint32_t*)(RKC + 64 * 11);  // the workgroup's parent-run counter
+    uint32_t* next_proof = next_parent + 1;               // fused proofs: next node (workgroup ordinal)
+    uint32_t* parent_done = next_parent + 8;              // fused proofs: parents whose child seeds are stored
     // the T-table lookups use the v_perm result as the absolute LDS address
     // (aes.hpp lds_read_asm): the table must start at LDS address 0
     if ((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)eval_lds != 0u) __builtin_trap();
@@ -708,13 +714,14 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             kc[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_conv + (size_t)i * S, lb));
         }
     }
-    if (threadIdx.x == 0) *next_parent = 0u;
+    if (threadIdx.x < EVAL_SYNC_WORDS) next_parent[threadIdx.x] = 0u;
     __syncthreads();
     const int aes_waves = a.aes_waves;
     // Proof waves: node proofs of level - 1 (children seeds from cs_in), then
     // they help with the parents; with no proofs to do (level 0, a frontier-
     // cache hit) they walk parents from the start.  No wave returns early: a
-    // cache hit's fused proofs below end with a workgroup barrier.
+    // cache hit's fused proofs below take nodes from every wave (and the A/B
+    // barrier schedule ends with a workgroup barrier).
     if (wave >= aes_waves && a.pv_nodes > 0 && !(a.dbg_skip & 1)) {
         if (a.proof_prio == 1) __builtin_amdgcn_s_setprio(1);
         if (a.proof_prio == 2) __builtin_amdgcn_s_setprio(2);
@@ -742,7 +749,49 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     // proofs are done, so no wave idles while another still has parents.
     const int wp0 = blockIdx.y * a.par_waves * a.ppw;
     const int wp1 = min(wp0 + a.par_waves * a.ppw, a.n_parents);
+    // Frontier-cache hit (FC, fuse_proofs == 1): THIS level's node proofs
+    // (vidpf.py:366-380, :321-323) of the workgroup's children, overlapped with
+    // its parents' AES.  The AES waves [0, aes_waves) walk the parents; a wave
+    // that has stored a parent's child seeds and control bits marks the parent
+    // in parent_done (release, workgroup scope).  The proof waves take the
+    // children in order through next_proof and wait (acquire) for their
+    // parent's mark; AES waves that run out of parents join them.  So some
+    // waves run the LDS-bound AES while others run the VALU-bound Keccak: with
+    // one workgroup per CU (150 KiB of LDS) the two pipes otherwise take turns
+    // (AES of every parent, barrier, proofs).  The host sizes the split by the
+    // two kinds' work per parent.  fuse_proofs == 3 (A/B only): the barrier
+    // schedule.  (Taking ready nodes inside the parent loop instead keeps the
+    // loop's state live across the Keccak: 74 spilled VGPRs, 769 scratch loads.)
+    const int pn_beg = 2 * wp0, pn_end = 2 * wp1;  // this workgroup's child nodes
+    const bool fuse_ovl = FC && a.fuse_proofs == 1;
+    auto parent_marked = [&](int q) -> bool {
+        const uint32_t w = __hip_atomic_load(parent_done + (q >> 5), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (__builtin_amdgcn_readfirstlane(w) >> (q & 31)) & 1u;
+    };
+    auto claim_node = [&]() -> int {
+        uint32_t o = 0;
+        if (lane == 0) o = atomicAdd(next_proof, 1u);
+        return pn_beg + (int)__builtin_amdgcn_readfirstlane(o);
+    };
+    auto node_proof_at = [&](int node) {
+        if (a.dbg_skip & 2) return;  // timing knob: no parents were evaluated
+        if (fuse_ovl)
+            while (!parent_marked((node - pn_beg) >> 1)) __builtin_amdgcn_s_sleep(2);
+        const int l = a.level;
+        uint32_t* ohg = a.cur_onehot + (size_t)blockIdx.x * a.oh_gstride;
+        const uint32_t lt = (uint32_t)lane * 4u;
+        uint32_t pcw[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)l * 8 + j) * S, lb);
+        uint32_t sd[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_out + ((size_t)node * 5 + i) * S, lb);
+        const uint32_t t = pld(a.cs_out + ((size_t)node * 5 + 4) * S, lb);
+        node_proof_one(a.np, a.np_f, p.bits, l, a.cur_path_bytes, sd, a.cur_child_path + node * 8, t, pcw,
+                       [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
+    };
     if (a.dbg_skip & 2) goto aes_done;
+    if (fuse_ovl && wave >= aes_waves) goto aes_done;  // proof waves of a hit
     {
     if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
     if (a.aes_prio == 2) __builtin_amdgcn_s_setprio(2);
@@ -959,6 +1008,14 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         // waitcnt pass keeps a vmcnt wait in the loop header (every block)
         __builtin_amdgcn_s_waitcnt(0x0F70);
 #endif
+        if constexpr (FC) {
+            if (fuse_ovl && lane == 0) {
+                // the child seeds / control bits above are stored: their proofs may start
+                const int q = pi - wp0;
+                __hip_atomic_fetch_or(parent_done + (q >> 5), 1u << (q & 31), __ATOMIC_RELEASE,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
         {
             // Fast path: block b (counter b + 1) of each child's convert stream
             // holds Field64 candidates 2b and 2b + 1, or Field128 candidate b
@@ -1044,28 +1101,11 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 aes_done:
     if constexpr (FC) {
         if (a.fuse_proofs) {
-            // frontier-cache hit: this level's node proofs (vidpf.py:366-380,
-            // :321-323) of the workgroup's children, once all its parents are
-            // done (the child seeds / control bits are in cs_out; the barrier
-            // orders the other waves' stores before these loads).  The VALU-
-            // bound Keccak of one workgroup overlaps the LDS-bound AES of the
-            // others on the CU, and no k_node_proof launch follows.
-            __syncthreads();
-            const int l = a.level;
-            const int nb = 2 * wp0, ne = 2 * wp1;
-            uint32_t* ohg = a.cur_onehot + (size_t)blockIdx.x * a.oh_gstride;
-            const uint32_t lt = (uint32_t)lane * 4u;
-            uint32_t pcw[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) pcw[j] = pld(pl.cw_proof + ((size_t)l * 8 + j) * S, lb);
-            for (int node = nb + wave; node < ne; node += EVAL_WAVES) {
-                uint32_t sd[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_out + ((size_t)node * 5 + i) * S, lb);
-                const uint32_t t = pld(a.cs_out + ((size_t)node * 5 + 4) * S, lb);
-                node_proof_one(a.np, a.np_f, p.bits, l, a.cur_path_bytes, sd, a.cur_child_path + node * 8, t, pcw,
-                               [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
-            }
+            // the nodes nobody has taken yet (overlapped: their parents may still
+            // be running; A/B barrier schedule: after every parent is done)
+            if (!fuse_ovl) __syncthreads();
+#pragma unroll 1
+            for (int node = claim_node(); node < pn_end; node = claim_node()) node_proof_at(node);
         }
     }
 }

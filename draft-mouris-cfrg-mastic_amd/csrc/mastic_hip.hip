@@ -177,6 +177,7 @@ struct mastic_ctx {
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
     int n_cus = 256;                     // compute units of the device
     int proof_waves = EVAL_PROOF_WAVES;  // proof waves per eval workgroup (MASTIC_PROOF_WAVES)
+    int hit_proof_waves = 0;             // ... of a fused-proof hit launch (0 = by the work split; MASTIC_HIT_PROOF_WAVES)
     int proof_prio = 0;                  // their s_setprio (MASTIC_PROOF_PRIO)
     int aes_prio = 0;                    // s_setprio of the AES waves (MASTIC_AES_PRIO)
     int dbg_skip = 0;                    // timing experiments only (MASTIC_DBG_SKIP; results wrong): 1 no node proofs, 2 no AES, 4 no binder sponges
@@ -205,8 +206,9 @@ struct mastic_ctx {
                hipStreamSynchronize(stream3) == hipSuccess;
     }
     bool fc_all = false;        // A/B only: the frontier-cache kernel variant at every level (MASTIC_FC_ALL=1)
-    int fuse_proofs = 1;        // last level's node proofs in the level kernel: 1 on cache hits, 2 also on
-                                // cache-on misses, 0 never (MASTIC_FUSE_PROOFS; else k_node_proof)
+    int fuse_proofs = 1;        // last level's node proofs in the level kernel, overlapped with its AES: 1 on
+                                // cache hits, 2 also on cache-on misses, 0 never (MASTIC_FUSE_PROOFS; else
+                                // k_node_proof); 3 (A/B): on hits, after a workgroup barrier
     size_t chunk_max = 0;        // reports per chunk cap (0 = what fits; MASTIC_CHUNK_REPORTS)
     bool chunk_pipeline = true;  // several chunks: two halves of the work arena (MASTIC_CHUNK_PIPELINE=0: off)
     int par_waves = 0;           // waves' worth of parents per level-kernel workgroup (0 = by field; MASTIC_PAR_WAVES)
@@ -596,6 +598,21 @@ static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst
     return 0;
 }
 
+// Proof waves of a level kernel whose node proofs are fused and overlapped
+// (a frontier-cache hit, kernels.hpp fuse_ovl): the proofs' share of the work
+// per parent, two Keccak-p (VALU, ~3.2k CU-cycles) against the AES of the
+// extend pair, the convert seeds, both children's payload blocks and the
+// parent-payload recompute, 4 + 3 nblk blocks (LDS: 2 x 133 cycles per block
+// at the kernel's ~50 % LDS efficiency).  C3 (Count): 7 of 16, the c2sweep
+// (Sum 255, 9 payload blocks): 3.
+static int hit_proof_waves(const McParams& p, const mastic_ctx* c) {
+    if (c->hit_proof_waves > 0) return c->hit_proof_waves;
+    const int epb = p.field == 64 ? 2 : 1;
+    const int nblk = (p.value_len + epb - 1) / epb;
+    const double K = 3170.0, A = (4.0 + 3.0 * nblk) * 532.0;
+    return std::max(1, std::min(12, (int)std::lround(EVAL_WAVES * K / (K + A))));
+}
+
 // One chunk of reports [base, base + n) of a prep_init, in work area W.
 // lc: the frontier cache (or null); on a hit the parents' seeds / payloads
 // are read from cin_cs / cin_w (the cache slot, or its predecessor when the
@@ -723,7 +740,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // the last level's node proofs in the level kernel (after each workgroup's
     // parents) instead of a k_node_proof launch: cache hits, and with
     // MASTIC_FUSE_PROOFS=2 cache-on misses too (whole parents only)
-    const bool fuse_last = hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs >= 2);
+    const bool fuse_last = hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs == 2);
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
         if (!hit && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
@@ -757,11 +774,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.wp_buf = plane(wl.fr_w[(l + 1) & 1]);
         a.recompute_wp = hit ? 1 : 0;
         const bool fuse = fuse_last && l == t->L;
-        a.fuse_proofs = fuse ? 1 : 0;
+        a.fuse_proofs = fuse ? (c->fuse_proofs == 3 ? 3 : 1) : 0;
         a.cur_path_bytes = (l + 1 + 7) / 8;
         a.cur_child_path = t->d_path.as<uint32_t>() + t->off[l] * 8;
         a.cur_onehot = oh_buf(l);
         a.aes_waves = EVAL_WAVES - c->proof_waves;
+        if (fuse && a.fuse_proofs == 1) a.aes_waves = EVAL_WAVES - hit_proof_waves(p, c);
         a.par_waves = par_waves;
         a.proof_prio = c->proof_prio;
         a.aes_prio = c->aes_prio;
@@ -769,7 +787,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         const int gy = (n_items + a.par_waves * a.ppw - 1) / (a.par_waves * a.ppw);
         a.pv_level = l - 1;
         a.pv_nodes = (l > 0 && !hit) ? 2 * t->n_parents[l - 1] : 0;  // hit: level L-1's proofs are cached
-        a.pv_npw = (a.pv_nodes + gy * c->proof_waves - 1) / (gy * c->proof_waves);
+        const int pw = EVAL_WAVES - a.aes_waves;  // proof waves of this launch
+        a.pv_npw = (a.pv_nodes + gy * pw - 1) / (gy * pw);
         a.pv_path_bytes = (l + 7) / 8;
         a.pv_child_path = l > 0 ? t->d_path.as<uint32_t>() + t->off[l - 1] * 8 : nullptr;
         a.pv_onehot = l > 0 ? oh_buf(l - 1) : nullptr;
@@ -1786,8 +1805,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (pw2) c->par_waves = std::max(1, std::min(EVAL_WAVES, atoi(pw2)));
         const char* cp = getenv("MASTIC_CHUNK_PIPELINE");
         if (cp) c->chunk_pipeline = cp[0] != '0';
+        const char* hpw = getenv("MASTIC_HIT_PROOF_WAVES");
+        if (hpw) c->hit_proof_waves = std::max(0, std::min(15, atoi(hpw)));
         const char* fp = getenv("MASTIC_FUSE_PROOFS");
-        if (fp) c->fuse_proofs = std::max(0, std::min(2, atoi(fp)));
+        if (fp) c->fuse_proofs = std::max(0, std::min(3, atoi(fp)));
         const char* fa = getenv("MASTIC_FC_ALL");
         if (fa) c->fc_all = fa[0] == '1';
         const char* cr = getenv("MASTIC_CHUNK_REPORTS");
