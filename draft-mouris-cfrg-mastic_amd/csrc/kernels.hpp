@@ -519,16 +519,17 @@ struct AesArgs {
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
     uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
     int force_slow_blk;  // test hook: the Field64 fast path hands over to the exact stream at this block (-1 = never)
-    // frontier cache (mastic_set_frontier_cache).  Last level of a prep_init: the convert seeds of
-    // ALL children (extend output after correction, the seed of convert) by child node index,
-    // staged for the cache.  Cache hit: the parents' payloads are recomputed from their cached
-    // convert seeds (cv_in, by node index, plus the control bit in cs_in) into wp_buf (by parent
-    // ordinal) instead of being cached: 16 B per node instead of VALUE_LEN field elements.
-    uint32_t* last_cv;
-    const uint32_t* cv_in;
+    // frontier cache (mastic_set_frontier_cache).  A cached node is 5 words: its convert seed (the
+    // extend output after correction, the seed of convert) and its control bit.  Last level of a
+    // prep_init: every child's node is written straight into the cache's spare slot (cache_out,
+    // plane stride cache_stride).  Cache hit: the parents come from the cache (cs_in, stride
+    // in_stride), and each parent's seed (block 0 of its convert stream) and payload (the rest of
+    // the stream, corrected) are recomputed, the payload into wp_buf by parent ordinal.
+    uint32_t* cache_out;
+    int cache_stride;
     uint32_t* wp_buf;
     int recompute_wp;
-    int in_stride;  // plane stride of cs_in / cv_in (the cache's, on a hit; else the work buffer's)
+    int in_stride;  // plane stride of cs_in (the cache's, on a hit; else the work buffer's)
     // frontier-cache hit (FC only): the AES waves also compute THIS level's
     // node proofs right after each parent's payloads (no k_node_proof launch)
     int fuse_proofs;
@@ -566,12 +567,25 @@ struct AesArgs {
 // stream takes over from that element.
 template <class F>
 MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[4], uint32_t t, const uint32_t* cw,
-                         int S, int r, int e_lo, int e_hi, uint32_t* out, int row0, int force_slow_blk) {
+                         int S, int r, int e_lo, int e_hi, uint32_t* out, int row0, int force_slow_blk,
+                         uint32_t seed_out[4]) {
     typedef typename F::E E;
     constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
     const int nblk = (e_hi + EPB - 1) / EPB;
     AesCtrGroup g;
-    uint32_t g_hi = ~0u;
+    uint32_t g_hi = 0u;
+    {
+        // the parent's seed: block 0 of the same stream (next(16), vidpf.py:352-364), in the
+        // counter group of the payload's first blocks
+        const uint32_t* const sd[1] = {cv};
+        const uint32_t hv[1] = {0u};
+        AesCtrGroup* const gi[1] = {&g};
+        ctr_group_init<1>(TL, rkc, sd, hv, gi);
+        const AesCtrGroup* const gg[1] = {&g};
+        const uint32_t c0v[1] = {0u};
+        uint32_t* const ov[1] = {seed_out};
+        ctr_blocks_n<1>(TL, rkc, gg, sd, c0v, ov);
+    }
     int e_fast = e_lo;
     auto put = [&](int e, E x) {
         if (t) x = F::add(x, pl_load<F>(cw, e, S, r));
@@ -853,13 +867,11 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         if (nxt >= 0) load_parent(nxt, nps, npctrl);
         if constexpr (FC) {
             if (a.recompute_wp) {
-                // frontier-cache hit: this parent's payload from its cached convert seed
-                const int pn = a.parent_node[pi];
-                uint32_t pcv[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) pcv[i] = pld(a.cv_in + ((size_t)pn * 4 + i) * S_in, lb);
+                // frontier-cache hit: ps holds this parent's cached convert seed; its payload
+                // and its seed (into ps) from the convert stream
+                const uint32_t pcv[4] = {ps[0], ps[1], ps[2], ps[3]};
                 parent_payload<F>(TL, rkc, pcv, pctrl, pl.cw_w + (size_t)(l - 1) * wl * S, S, r, e_lo, e_hi, a.wp_buf,
-                                  pi * vl, a.force_slow_blk);
+                                  pi * vl, a.force_slow_blk, ps);
                 // the children's loop below reads these elements back (same lanes)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
@@ -919,14 +931,17 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
 #endif
         if constexpr (FC) {
-            if (a.last_cv) {
-                // convert seeds of the last level's children, staged for the frontier cache
-                const size_t n0 = (size_t)(2 * pi) * 4, n1 = n0 + 4;
+            if (a.cache_out) {
+                // the last level's children as frontier-cache nodes: convert seed, control bit
+                const int CS = a.cache_stride;
+                const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    pst(a.last_cv + (n0 + i) * S, lb, cs0[i]);
-                    pst(a.last_cv + (n1 + i) * S, lb, cs1[i]);
+                    pst(a.cache_out + (n0 + i) * CS, lb, cs0[i]);
+                    pst(a.cache_out + (n1 + i) * CS, lb, cs1[i]);
                 }
+                pst(a.cache_out + (n0 + 4) * CS, lb, tc0);
+                pst(a.cache_out + (n1 + 4) * CS, lb, tc1);
             }
         }
         {

@@ -102,15 +102,16 @@ inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 // the whole tree again, but its levels 0..L-1 are usually exactly the previous
 // call's tree.  The cache keeps, per report, the two binder sponges' states
 // after the cached call's levels (the binder messages are BFS-ordered, so the
-// cached message is a prefix of the next one), the last level's child seeds /
-// control bits and payloads, and the root sum; a call whose tree extends the
-// cached one by one level evaluates and absorbs only that level.
+// cached message is a prefix of the next one), every node of the last level as
+// its convert seed and control bit (5 words: a hit recomputes a parent's seed
+// and payload from its convert stream), and the root sum; a call whose tree
+// extends the cached one by one level evaluates and absorbs only that level.
 // Planes of all n reports (stride S, independent of the HBM-budget chunks a
-// call runs in, so a sweep's chunking may change from level to level); one
-// slot per aggregator: a hit reads its parents from the slot before the same
-// chunk's new level is copied over them (stream order), and a slot that must
-// grow is replaced by a larger one whose predecessor is retired only after
-// the call (mastic_ctx::graveyard).
+// call runs in, so a sweep's chunking may change from level to level).  The
+// last level kernel writes its children straight into a spare node slot
+// shared by the ctx's aggregators (mastic_ctx::fc_spare; a hit reads its
+// parents from this aggregator's slot meanwhile), and the call then swaps the
+// two: three node slots in all, no copy of the level into the cache.
 struct LevelCache {
     bool valid = false;
     uint64_t rep_id = 0, rep_gen = 0;  // the batch (mastic_reports::id) and its contents generation
@@ -121,15 +122,14 @@ struct LevelCache {
     std::vector<int> n_parents;                 // per level 0..L
     std::vector<uint32_t> paths;                // child paths of level L (8 words per node)
     DevBuf sp, rootsum;                         // both binder sponges (2 x 50 planes); root sum (wl planes)
-    DevBuf cs, cv;                              // last level: seeds / ctrl [node][5], convert seeds [node][4]
-    size_t nodes_cap = 0;                       // nodes cs / cv can hold
+    DevBuf nd;                                  // last level's nodes [node][5]: convert seed, control bit
+    size_t nodes_cap = 0;                       // nodes nd can hold
     void drop() { valid = false; }
     void release() {
         drop();
         sp.release();
         rootsum.release();
-        cs.release();
-        cv.release();
+        nd.release();
         nodes_cap = 0;
         S = 0;
     }
@@ -219,6 +219,9 @@ struct mastic_ctx {
     bool frontier_cache = false;  // mastic_set_frontier_cache
     bool last_hit = false;        // the last prep_init evaluated only its last level
     LevelCache lc[2];
+    DevBuf fc_spare;          // the frontier cache's spare node slot (LevelCache::nd layout)
+    size_t spare_cap = 0;     // nodes it can hold
+    size_t spare_S = 0;       // its plane stride
     std::vector<void*> graveyard;  // replaced cache slots, freed once the streams are idle
     void bury() {
         for (void* q : graveyard) (void)hipFree(q);
@@ -458,13 +461,11 @@ struct WorkLayout {
     size_t words = 0;  // per report (plane count)
     size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
         rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, cs[2], fr_w[2], onehot[3],
-        payload[3], out, lastcv;
+        payload[3], out;
 };
 static constexpr int NSLOT = 3;  // level buffers in flight between eval and absorb
 
-// cache: the frontier cache is on (the last level's convert seeds of every
-// node are staged in the work buffer before they are copied into the cache)
-static WorkLayout work_layout(const McParams& p, const Tree* t, bool cache = false) {
+static WorkLayout work_layout(const McParams& p, const Tree* t) {
     WorkLayout w;
     size_t o = 0;
     auto take = [&](size_t n) {
@@ -505,7 +506,6 @@ static WorkLayout work_layout(const McParams& p, const Tree* t, bool cache = fal
         w.payload[k] = take((size_t)t->max_parents * wl);
     }
     w.out = take((size_t)std::max(t->n_prefixes, 1) * (1 + p.output_len) * p.w32);
-    w.lastcv = take(cache ? (size_t)2 * t->n_parents[t->L] * 4 : 0);
     w.words = o;
     return w;
 }
@@ -614,17 +614,17 @@ static int hit_proof_waves(const McParams& p, const mastic_ctx* c) {
 }
 
 // One chunk of reports [base, base + n) of a prep_init, in work area W.
-// lc: the frontier cache (or null); on a hit the parents' seeds / payloads
-// are read from cin_cs / cin_w (the cache slot, or its predecessor when the
-// slot grew).  tail: the stream of the chunk's last part (finalize, FLP,
+// lc: the frontier cache (or null); on a hit the parents are read from
+// cin (the aggregator's node slot); the last level's nodes go to cout (the
+// spare slot).  tail: the stream of the chunk's last part (finalize, FLP,
 // result and cache copies): the sponge stream when chunks are pipelined (the
 // next chunk's evaluation, in the other half of the work arena, then
 // overlaps this chunk's last sponges), else the main stream.  sev0: first
 // sync event of this chunk (consecutive pipelined chunks use disjoint ones).
 template <class F>
 static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const WorkLayout& wl, int agg_id,
-                     size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit, const uint32_t* cin_cs,
-                     const uint32_t* cin_cv, uint32_t* W, hipStream_t ss, hipStream_t tail, size_t sev0) {
+                     size_t base, int n, int stride, size_t& evi, LevelCache* lc, bool hit, const uint32_t* cin,
+                     uint32_t* cout, uint32_t* W, hipStream_t ss, hipStream_t tail, size_t sev0) {
     const McParams& p = c->p;
     Planes pl = make_planes(W, wl, n, stride);
     // Every level plane (child seeds, frontier payloads, proof / payload-
@@ -758,7 +758,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.parent_node = t->d_parent.as<int32_t>() + t->poff[l];
         a.child_exp = t->d_exp.as<int32_t>() + t->off[l];
         a.child_pfx = t->d_pfx.as<int32_t>() + t->off[l];
-        a.cs_in = hit ? cin_cs + base : plane(wl.cs[(l + 1) & 1]);
+        a.cs_in = hit ? cin + base : plane(wl.cs[(l + 1) & 1]);
         a.cs_out = plane(wl.cs[l & 1]);
         a.fr_w_in = plane(wl.fr_w[(l + 1) & 1]);
         a.in_stride = hit ? (int)lc->S : stride;
@@ -769,8 +769,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // frontier cache: stage this level's convert seeds (last level); on a
         // hit recompute the parents' payloads from the cached ones into the
         // (otherwise unused) parent-payload planes
-        a.last_cv = (lc && l == t->L) ? plane(wl.lastcv) : nullptr;
-        a.cv_in = hit ? cin_cv + base : nullptr;
+        a.cache_out = (lc && l == t->L) ? cout + base : nullptr;
+        a.cache_stride = lc ? (int)lc->S : 0;
         a.wp_buf = plane(wl.fr_w[(l + 1) & 1]);
         a.recompute_wp = hit ? 1 : 0;
         const bool fuse = fuse_last && l == t->L;
@@ -883,11 +883,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     }
     HIPCHK(c, hipGetLastError());
     if (lc) {
-        // frontier cache for the next level: last level's seeds/ctrl and convert seeds, root sum.
-        // Stream order: this chunk's level kernel has read its parents from the slot.
-        const size_t nl = (size_t)2 * t->n_parents[t->L];
-        if (to_cache(lc->cs.as<uint32_t>(), plane(wl.cs[t->L & 1]), nl * 5)) return -1;
-        if (to_cache(lc->cv.as<uint32_t>(), plane(wl.lastcv), nl * 4)) return -1;
+        // frontier cache for the next level (the last level's nodes are in the
+        // spare slot already, written by its level kernel): the root sum
         if (!hit && to_cache(lc->rootsum.as<uint32_t>(), pl.rootsum, (size_t)wlw)) return -1;
         // both sponges after levels 0..L (stream waited for abs_done[L] above)
         if (to_cache(lc->sp.as<uint32_t>(), pl.sp_onehot, 50)) return -1;
@@ -983,8 +980,8 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     // the slot before the work buffer, so the HBM budget sees the cache
     LevelCache* lc = nullptr;
     bool hit = false;
-    const uint32_t *cin_cs = nullptr, *cin_cv = nullptr;
-    std::vector<void*> retire_after;  // slot buffers the hit still reads
+    const uint32_t* cin = nullptr;  // a hit's parents: this aggregator's node slot
+    uint32_t* cout = nullptr;       // the last level's nodes: the spare node slot
     std::vector<uint8_t> lkey(1, (uint8_t)vk_len);
     lkey.insert(lkey.end(), verify_key, verify_key + vk_len);
     lkey.insert(lkey.end(), app_ctx, app_ctx + ctx_len);
@@ -1008,10 +1005,14 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         if (lc->S != S1) {
             retire(lc->sp);
             retire(lc->rootsum);
-            retire(lc->cs);
-            retire(lc->cv);
+            retire(lc->nd);
             lc->nodes_cap = 0;
             lc->S = S1;
+        }
+        if (c->spare_S != S1) {
+            retire(c->fc_spare);
+            c->spare_cap = 0;
+            c->spare_S = S1;
         }
         const size_t wlw = (size_t)p.value_len * p.w32;
         const size_t nl = (size_t)2 * t->n_parents[L];
@@ -1025,56 +1026,38 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
             return b.ensure(bytes);
         };
         bool ok = alloc(lc->sp, 100 * S1 * 4) && alloc(lc->rootsum, wlw * S1 * 4);
-        if (ok && nl > lc->nodes_cap) {
+        if (ok && nl > c->spare_cap) {
             // grow geometrically (a sweep's frontier widens over several
             // levels), and while HBM is plentiful straight to up to 4x the
             // need within a fifth of the free memory: each large hipMalloc
             // costs ~1 s per 50 GB, so a 1M-report sweep should grow its
             // slots a couple of times, not at every level
-            size_t cap = std::max(nl, lc->nodes_cap + lc->nodes_cap / 4);
+            size_t cap = std::max(nl, c->spare_cap + c->spare_cap / 4);
             size_t freeb = 0, totalb = 0;
             if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-                const size_t per_node = (5 + 4) * S1 * 4;
+                const size_t per_node = 5 * S1 * 4;
                 cap = std::max(cap, std::min(4 * nl, freeb / 5 / per_node));
             }
-            DevBuf ncs, ncv;
-            if (!c->graveyard.empty()) {  // the other aggregator's retired slot: free it first
-                if (c->idle()) c->bury();
-            }
-            ok = alloc(ncs, cap * 5 * S1 * 4) && alloc(ncv, cap * 4 * S1 * 4);
-            if (ok) {
-                if (hit) {
-                    cin_cs = lc->cs.as<uint32_t>();
-                    cin_cv = lc->cv.as<uint32_t>();
-                    retire_after = {lc->cs.p, lc->cv.p};
-                    lc->cs.p = lc->cv.p = nullptr;
-                    lc->cs.bytes = lc->cv.bytes = 0;
-                } else {
-                    retire(lc->cs);
-                    retire(lc->cv);
-                }
-                std::swap(lc->cs.p, ncs.p);
-                std::swap(lc->cs.bytes, ncs.bytes);
-                std::swap(lc->cv.p, ncv.p);
-                std::swap(lc->cv.bytes, ncv.bytes);
-                lc->nodes_cap = cap;
-            }
+            // the spare may be a former slot that queued kernels still read:
+            // retire it, and free the retired buffers first
+            retire(c->fc_spare);
+            c->spare_cap = 0;
+            if (c->idle()) c->bury();
+            ok = alloc(c->fc_spare, cap * 5 * S1 * 4);
+            if (ok) c->spare_cap = cap;
         }
         if (!ok) {  // not enough HBM for the cache: evaluate without it
-            for (void* q : retire_after) c->graveyard.push_back(q);
-            retire_after.clear();
             lc->release();
             lc = nullptr;
             hit = false;
-        } else if (hit && !cin_cs) {
-            cin_cs = lc->cs.as<uint32_t>();
-            cin_cv = lc->cv.as<uint32_t>();
+        } else {
+            cin = hit ? lc->nd.as<uint32_t>() : nullptr;
+            cout = c->fc_spare.as<uint32_t>();
         }
         if (!hit && lc) lc->drop();  // refilled by this call
     } else {
         c->lc[agg_id].drop();
     }
-    if (lc) wl = work_layout(p, t, true);
     // with the cache on, half of the free HBM: the other aggregator's slot may
     // still grow at this level
     const uint64_t budget = (lc && !c->budget) ? default_budget(c) * 2 / 3 : default_budget(c);
@@ -1142,12 +1125,11 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         hipStream_t ss = (pipe && h) ? c->stream3 : c->stream2;
         hipStream_t tail = pipe ? ss : c->stream;
         rc = p.field == 64
-                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_cv, W, ss, tail,
+                 ? run_chunk<F64>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin, cout, W, ss, tail,
                                   h * nsev)
-                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin_cs, cin_cv, W, ss, tail,
+                 : run_chunk<F128>(c, rep, t, wl, agg_id, b, nn, stride, evi, lc, hit, cin, cout, W, ss, tail,
                                    h * nsev);
         if (rc) {
-            for (void* q : retire_after) c->graveyard.push_back(q);
             if (lc) lc->drop();
             return rc;
         }
@@ -1161,8 +1143,13 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
         HIPCHK(c, hipStreamWaitEvent(c->stream, done, 0));
         HIPCHK(c, hipStreamWaitEvent(c->stream, done3, 0));
     }
-    for (void* q : retire_after) c->graveyard.push_back(q);
     if (lc) {
+        // the spare slot now holds this call's last level: it becomes the
+        // aggregator's slot, and the old slot (read by this call's hit) the
+        // spare, overwritten only by later calls' kernels (stream order)
+        std::swap(lc->nd.p, c->fc_spare.p);
+        std::swap(lc->nd.bytes, c->fc_spare.bytes);
+        std::swap(lc->nodes_cap, c->spare_cap);
         lc->valid = true;
         lc->rep_id = rep->id;
         lc->rep_gen = rep->generation();
@@ -1729,7 +1716,13 @@ extern "C" int mastic_reports_shard(mastic_reports* rep, const uint8_t* app_ctx,
     if (!rep) return MASTIC_EINVAL;
     mastic_ctx* c = rep->ctx;
     rep->touch();
-    if (rep->n == 0) return 0;
+    if (rep->n == 0) {
+        // an empty batch holds both aggregators' (zero) input shares, so that
+        // prep_init accepts it and its views (e.g. a rank of a split job that
+        // gets no reports)
+        if (!rep->in0.ensure(0) || !rep->in1.ensure(0)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        return 0;
+    }
     if (!alphas || !nonces || !rands || (!betas && c->p.meas_len > 0)) return fail(c, MASTIC_EINVAL, "null input");
     int rc = build_prefixes(c, app_ctx, ctx_len, nullptr, 0);
     if (rc) return rc;
@@ -1868,13 +1861,18 @@ extern "C" int mastic_set_frontier_cache(mastic_ctx* c, int on, int* last_hit) {
             // queued kernels may still read the cache slots: retire them (freed
             // at the next idle point of the ctx's streams), no synchronisation
             for (auto& x : c->lc) {
-                for (DevBuf* b : {&x.sp, &x.rootsum, &x.cs, &x.cv}) {
+                for (DevBuf* b : {&x.sp, &x.rootsum, &x.nd}) {
                     if (b->p && b->own) c->graveyard.push_back(b->p);
                     b->p = nullptr;
                     b->bytes = 0;
                 }
                 x.release();
             }
+            if (c->fc_spare.p && c->fc_spare.own) c->graveyard.push_back(c->fc_spare.p);
+            c->fc_spare.p = nullptr;
+            c->fc_spare.bytes = 0;
+            c->spare_cap = 0;
+            c->spare_S = 0;
         }
     }
     if (last_hit) *last_hit = c->last_hit ? 1 : 0;

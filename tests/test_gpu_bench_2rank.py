@@ -37,7 +37,9 @@ def _run_bench(args, timeout=500):
     env = dict(os.environ, MASTIC_BENCH_BACKEND="gloo", MASTIC_BENCH_DEVICE="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
                        text=True, timeout=timeout)
-    assert r.returncode == 0, r.stderr[-3000:]
+    # the failing rank's own traceback, not only the launcher's tail
+    first = "\n".join(l for l in r.stderr.splitlines() if l.startswith("[rank0]") or "Error" in l)[:4000]
+    assert r.returncode == 0, first + "\n...\n" + r.stderr[-1500:]
     return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
 
 

@@ -420,6 +420,25 @@ def test_empty_batch(mastic_amd):
     assert [x.int() for x in agg] == [0] * (2 * (1 + m.OUTPUT_LEN))
 
 
+def test_empty_sharded_batch_and_view(mastic_amd):
+    """A device batch sharded from zero reports (a rank of a split job that
+    gets none) and a zero-report view of it run prep_init for both
+    aggregators, decide and fold like any other batch."""
+    m = mastic_amd.MasticSum(6, 7)
+    ap = (5, ((True,) * 6, (False,) * 6), True)
+    dev = m.reports_shard(CTX, b"", b"", b"", b"")
+    assert dev.n == 0
+    for batch in (dev, dev.view(0, 0)):
+        for agg_id in range(2):
+            m.prep_init_device(batch, bytes(16), CTX, agg_id, ap)
+            (ps, _js, out, st) = m.prep_result(batch, agg_id, ap, want_out_shares=True)
+            assert ps == b"" and out == b"" and len(st) == 0
+        (acc, _codes) = m.decide_results(CTX, 0)
+        assert len(acc) == 0
+        agg = m.aggregate_device(1, ap)
+        assert [x.int() for x in agg] == [0] * (2 * (1 + m.OUTPUT_LEN))
+
+
 def test_empty_prefix_list_rejected(mastic_amd):
     """The poc cannot evaluate an empty candidate set (mastic.py:270 reads the
     root's unset children); the GPU path refuses it with ValueError."""
