@@ -169,19 +169,7 @@ def agg_param_bytes(level, attrs):
 # ---------------------------------------------------------------- CPU baseline
 def _cpu_worker(job):
     (spec, enc_ap, nonce, pub, ins, vk, ctx, agg_id) = job
-    sys.path.insert(0, ROOT)
-    from oracle import mastic as om
-    (circuit, kw) = spec
-    kw = dict(kw)
-    bits = kw.pop("bits")
-    if circuit == "Sum":
-        o = om.MasticSum(bits, kw["max_measurement"])
-    elif circuit == "Count":
-        o = om.MasticCount(bits)
-    elif circuit == "Histogram":
-        o = om.MasticHistogram(bits, kw["length"], kw["chunk_length"])
-    else:
-        o = om.MasticSumVec(bits, kw["length"], kw["sum_vec_bits"], kw["chunk_length"])
+    o = _oracle_mastic(*spec)
     ap = o.decode_agg_param(enc_ap)
     cws = o.vidpf.decode_public_share(pub)
     isd = o.decode_input_share(agg_id, ins)
@@ -189,6 +177,51 @@ def _cpu_worker(job):
     (_st, sh) = o.prep_init(vk, ctx, agg_id, ap, nonce, cws, isd)
     dt = time.perf_counter() - t
     return (dt, o.test_vec_encode_prep_share(sh))
+
+
+def _oracle_mastic(circuit, kw):
+    sys.path.insert(0, ROOT)
+    from oracle import mastic as om
+    kw = dict(kw)
+    bits = kw.pop("bits")
+    if circuit == "Sum":
+        return om.MasticSum(bits, kw["max_measurement"])
+    if circuit == "Count":
+        return om.MasticCount(bits)
+    if circuit == "Histogram":
+        return om.MasticHistogram(bits, kw["length"], kw["chunk_length"])
+    return om.MasticSumVec(bits, kw["length"], kw["sum_vec_bits"], kw["chunk_length"])
+
+
+def native_cpu_point(m, cfg, enc_ap, reps, vk, ctx, agg_id, threads, n_prefixes, per_thread=2):
+    """The native multithreaded CPU baseline (oracle/native_prep.c: AES-NI,
+    64-bit Keccak, one thread per report range; the FLP query in the Python
+    oracle): prep_init of per_thread reports per thread of the same workload,
+    timed on the host, its prep shares checked against the GPU's."""
+    sys.path.insert(0, ROOT)
+    from oracle.native import has_aesni, prep_init_native
+    nn = min(per_thread * threads, reps.n)
+    (rn, pub, in0, in1) = reps.view(0, nn).download()
+    ins = in0 if agg_id == 0 else in1
+    o = _oracle_mastic(cfg["circuit"], cfg["kw"])
+    ap = o.decode_agg_param(enc_ap)
+    t = time.perf_counter()
+    (shares, _outs) = prep_init_native(o, vk, ctx, agg_id, ap, rn, pub, ins, threads)
+    wall = time.perf_counter() - t
+    (gps, _js, _o, _st) = m.prep_init_batch(vk, ctx, agg_id, enc_ap, rn, pub, ins, want_out_shares=False)
+    psz = m.prep_share_size(ap[2])
+    parity = all(gps[psz * i:psz * (i + 1)] == shares[i] for i in range(nn))
+    return {
+        "value": nn * n_prefixes / wall,
+        "unit": "report*prefix/s",
+        "cores": threads,
+        "kind": "port",
+        "impl": "native C (oracle/native_prep.c): AES-NI %s, 64-bit Keccak-p, pthreads; FLP query in the Python "
+                "oracle" % ("on" if has_aesni() else "off (byte-wise AES)"),
+        "sample": "%d reports x %d prefixes on %d threads (%d per thread), %.2f s; GPU/CPU prep shares "
+                  "bit-identical: %s" % (nn, n_prefixes, threads, per_thread, wall, parity),
+        "parity": parity,
+    }
 
 
 def cpu_baseline(jobs, procs):
@@ -601,6 +634,32 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         }
         out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
+        # the native multithreaded CPU point at the same levels (8 reports per thread)
+        nat_t, nat_u, nat_ok = 0.0, 0, True
+        nn = min(8 * procs, reps.n)
+        (nrn, npub, nin0, _nin1) = reps.view(0, nn).download()
+        sys.path.insert(0, ROOT)
+        from oracle.native import has_aesni, prep_init_native
+        o = _oracle_mastic(cfg["circuit"], cfg["kw"])
+        for lv in lvls:
+            ap = (lv.level, tuple(lv.prefixes), lv.level == 0)
+            t = time.perf_counter()
+            (nsh, _o) = prep_init_native(o, vk, ctx, 0, ap, nrn, npub, nin0, procs)
+            nat_t += time.perf_counter() - t
+            nat_u += nn * len(lv.prefixes)
+            enc_ap = m.encode_agg_param(ap)
+            (gps, _js, _o2, _st) = m.prep_init_batch(vk, ctx, 0, enc_ap, nrn, npub, nin0, want_out_shares=False)
+            psz = m.prep_share_size(ap[2])
+            nat_ok = nat_ok and all(gps[psz * i:psz * (i + 1)] == nsh[i] for i in range(nn))
+        out["cpu_baseline"]["native"] = {
+            "value": nat_u / nat_t, "unit": "report*prefix/s", "cores": procs, "kind": "port",
+            "impl": "native C (oracle/native_prep.c): AES-NI %s, 64-bit Keccak-p, pthreads; FLP query in the "
+                    "Python oracle" % ("on" if has_aesni() else "off"),
+            "sample": "%d reports x leader prep_init at levels %s (the sweep's candidate lists) on %d threads, "
+                      "%.2f s; GPU/CPU prep shares bit-identical: %s" % (nn, [lv.level for lv in lvls], procs,
+                                                                           nat_t, nat_ok),
+            "parity": nat_ok,
+        }
     del reps
     if rank == 0 and emit:
         if args.lib:
@@ -950,6 +1009,9 @@ def main():
         }
         out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
+        nat = native_cpu_point(m, cfg, enc_ap, reps_all, vk, ctx, args.agg_id, procs, len(attrs))
+        nat["gpu_over_native_cpu"] = out["value"] / nat["value"]
+        out["cpu_baseline"]["native"] = nat
     ns = None
     if args.config == "c2" and args.north_star:
         # the north_star job (BASELINE.json): bit-exact prep_init + aggregate for
@@ -1007,6 +1069,10 @@ def main():
                 out["north_star"]["speedup_spec_literal_vs_cpu_core"] = lit / cb["single_process_value"]
             out["north_star"]["speedup_cached_vs_cpu_pool"] = ns["value"] / cb["value"]
             out["north_star"]["speedup_cached_vs_cpu_core"] = ns["value"] / cb["single_process_value"]
+            if "native" in cb:
+                out["north_star"]["cpu_baseline"]["native"] = cb["native"]
+                if lit:
+                    out["north_star"]["speedup_spec_literal_vs_native_cpu"] = lit / cb["native"]["value"]
     if rank == 0:
         if args.lib:
             out["library"] = "alternate build (A/B only): " + args.lib
