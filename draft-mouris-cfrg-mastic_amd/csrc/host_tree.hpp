@@ -98,18 +98,23 @@ inline int tree_parse(int bits, const uint8_t* enc, size_t len, TreeShape* t, st
         }
         // nodes before any allocation: level l has 2 x (runs at length l) nodes,
         // runs at length l = 1 + #{s : lcp[s] < l}
+        uint64_t all_nodes = 0;
         {
             std::vector<uint64_t> below(level + 2, 0);  // below[m] = #{s >= 1 : lcp[s] < m}
             for (int s = 1; s < n; s++) below[std::min(lcp[s] + 1, level + 1)]++;
-            uint64_t runs = 0, total = 0;
+            uint64_t runs = 0;
             for (int l = 0; l <= level; l++) {
                 runs += below[l];
-                total += 2 * (1 + runs);
-                if (total > TREE_MAX_NODES) return tree_fail(err, TREE_ENOMEM, "agg param tree too large");
+                all_nodes += 2 * (1 + runs);
+                if (all_nodes > TREE_MAX_NODES) return tree_fail(err, TREE_ENOMEM, "agg param tree too large");
             }
         }
         TreeShape& T = *t;
         T = TreeShape();
+        T.child_exp.resize(all_nodes);
+        T.child_pfx.resize(all_nodes);
+        T.child_path.resize(8 * all_nodes);
+        T.parent_node.reserve(all_nodes / 2);
         T.L = level;
         T.n_prefixes = n;
         T.weight_check = enc[len - 1] == 1;
@@ -141,11 +146,15 @@ inline int tree_parse(int bits, const uint8_t* enc, size_t len, TreeShape* t, st
             }
             T.n_exp.push_back(n_next);
             T.off.push_back(total);
-            const int nb = (l + 1 + 7) / 8;  // path bytes at this level (<= 32: bits <= 256)
             for (int pi = 0; pi < np; pi++) {
                 const int b = run_begin[pi];
                 const int e = pi + 1 < np ? run_begin[pi + 1] : n;
                 const uint8_t* rep = P(order[b]);
+                // the parent's path: the run's first l bits (MSB-first bytes,
+                // bits past l zero); word k holds bytes 4k..4k+3 little-endian
+                uint8_t pb[32] = {0};
+                std::memcpy(pb, rep, (size_t)(l / 8));
+                if (l % 8) pb[l / 8] = (uint8_t)(rep[l / 8] & (0xFF00u >> (l % 8)));
                 for (int cbit = 0; cbit < 2; cbit++) {
                     // child cbit exists iff the run's first (cbit 0) / last (cbit 1)
                     // member has that bit at position l
@@ -158,18 +167,15 @@ inline int tree_parse(int bits, const uint8_t* enc, size_t len, TreeShape* t, st
                         else
                             cp = order[m];
                     }
-                    T.child_exp.push_back(ce);
-                    T.child_pfx.push_back(cp);
+                    const size_t node = total + 2 * (size_t)pi + cbit;
+                    T.child_exp[node] = ce;
+                    T.child_pfx[node] = cp;
                     // path: the parent's l bits, then cbit (bits past l + 1 zero)
-                    uint32_t w[8] = {0};
-                    for (int bi = 0; bi < nb; bi++) {
-                        uint32_t byte = rep[bi];
-                        const int lo = bi * 8;
-                        if (lo + 8 > l) byte = lo >= l ? 0u : (byte & ((0xFF00u >> (l - lo)) & 0xFFu));
-                        if (cbit && bi == l / 8) byte |= 0x80u >> (l % 8);
-                        w[bi / 4] |= byte << (8 * (bi % 4));
-                    }
-                    for (int k = 0; k < 8; k++) T.child_path.push_back(w[k]);
+                    if (cbit) pb[l / 8] |= (uint8_t)(0x80u >> (l % 8));
+                    uint32_t* w = T.child_path.data() + 8 * node;
+                    for (int k = 0; k < 8; k++)
+                        w[k] = (uint32_t)pb[4 * k] | (uint32_t)pb[4 * k + 1] << 8 | (uint32_t)pb[4 * k + 2] << 16 |
+                               (uint32_t)pb[4 * k + 3] << 24;
                 }
             }
             total += 2 * (size_t)np;

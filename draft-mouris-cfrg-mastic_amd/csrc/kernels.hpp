@@ -178,8 +178,10 @@ __global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_i
 
 // ------------------------------------------------------------- key setup
 // The two fixed AES keys of a report depend only on (ctx, usage, nonce)
-// (vdaf_poc XofFixedKeyAes128): derive them once, expand once.
-__global__ __launch_bounds__(256) void k_setup(Planes pl, const PrefixState* pfx) {
+// (vdaf_poc XofFixedKeyAes128): derive them once, expand once.  sponges:
+// also start both binder sponges (not on a frontier-cache hit, which resumes
+// them from the cache's planes).
+__global__ __launch_bounds__(256) void k_setup(Planes pl, const PrefixState* pfx, int sponges) {
     __shared__ uint32_t T[AES_LDS_WORDS];
     aes_lds_fill(T, threadIdx.x, 256);
     __syncthreads();
@@ -200,6 +202,7 @@ __global__ __launch_bounds__(256) void k_setup(Planes pl, const PrefixState* pfx
 #pragma unroll
         for (int i = 0; i < 44; i++) dst[i * S + r] = rk[i];
     }
+    if (!sponges) return;
     KState s;
     int f;
     load_prefix(pfx, PFX_ONEHOT, s, f);
@@ -517,7 +520,8 @@ struct AesArgs {
     const uint32_t* fr_w_in;     // payloads of level-1's expanded nodes [e][vl*w32]
     uint32_t* fr_w_out;
     uint32_t* payload;   // [n_parents * vl*w32]  w_p - w_L - w_R of the parents (BFS order)
-    uint32_t* out;       // [n_prefixes * (1 + out_len) * w32]
+    uint32_t* out;       // [n_prefixes * (1 + out_len) * w32] planes of the result buffer (row stride out_stride)
+    int out_stride;
     int force_slow_blk;  // test hook: the Field64 fast path hands over to the exact stream at this block (-1 = never)
     // frontier cache (mastic_set_frontier_cache).  A cached node is 5 words: its convert seed (the
     // extend output after correction, the seed of convert) and its control bit.  Last level of a
@@ -984,8 +988,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             if (GEN && (pf0 >= 0 || pf1 >= 0)) {
                 // truncated out share, negated for the helper (vidpf.py:259, mastic.py:311-314)
                 if (e == 0) {
-                    if (pf0 >= 0) pl_store<F>(a.out, pf0 * row, S, r, a.agg_id ? F::neg(x0) : x0);
-                    if (pf1 >= 0) pl_store<F>(a.out, pf1 * row, S, r, a.agg_id ? F::neg(x1) : x1);
+                    if (pf0 >= 0) pl_store<F>(a.out, pf0 * row, a.out_stride, r, a.agg_id ? F::neg(x0) : x0);
+                    if (pf1 >= 0) pl_store<F>(a.out, pf1 * row, a.out_stride, r, a.agg_id ? F::neg(x1) : x1);
                 } else if (e - 1 < p.tlimit) {
                     const int m = e - 1;
                     const int g = m % p.tgroup;
@@ -999,8 +1003,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                     }
                     if (g == p.tgroup - 1) {
                         const int o = 1 + m / p.tgroup;
-                        if (pf0 >= 0) pl_store<F>(a.out, pf0 * row + o, S, r, a.agg_id ? F::neg(acc0) : acc0);
-                        if (pf1 >= 0) pl_store<F>(a.out, pf1 * row + o, S, r, a.agg_id ? F::neg(acc1) : acc1);
+                        if (pf0 >= 0) pl_store<F>(a.out, pf0 * row + o, a.out_stride, r, a.agg_id ? F::neg(acc0) : acc0);
+                        if (pf1 >= 0) pl_store<F>(a.out, pf1 * row + o, a.out_stride, r, a.agg_id ? F::neg(acc1) : acc1);
                     }
                 }
             }

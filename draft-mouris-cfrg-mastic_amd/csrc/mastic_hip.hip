@@ -461,7 +461,7 @@ struct WorkLayout {
     size_t words = 0;  // per report (plane count)
     size_t key, nonce, cw_seed, cw_ctrl, cw_w, cw_proof, lps, seed, peer, rk_ext, rk_conv, sp_onehot, sp_payload,
         rootsum, beta, eval_proof, proof, qr, jr, jr_part, jr_seed, verifier, status, cs[2], fr_w[2], onehot[3],
-        payload[3], out;
+        payload[3];
 };
 static constexpr int NSLOT = 3;  // level buffers in flight between eval and absorb
 
@@ -505,7 +505,6 @@ static WorkLayout work_layout(const McParams& p, const Tree* t) {
         w.onehot[k] = take((size_t)t->max_level_nodes * 8);
         w.payload[k] = take((size_t)t->max_parents * wl);
     }
-    w.out = take((size_t)std::max(t->n_prefixes, 1) * (1 + p.output_len) * p.w32);
     w.words = o;
     return w;
 }
@@ -627,6 +626,16 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                      uint32_t* cout, uint32_t* W, hipStream_t ss, hipStream_t tail, size_t sev0) {
     const McParams& p = c->p;
     Planes pl = make_planes(W, wl, n, stride);
+    Result& R = c->res[agg_id];
+    // A single-chunk call with the frontier cache keeps both binder sponges
+    // and the root sum in the cache's planes (same stride): a hit resumes and
+    // updates them in place, a miss fills them; no copies in or out.
+    const bool direct = lc && base == 0 && (size_t)n == rep->n && lc->S == (size_t)stride;
+    if (direct) {
+        pl.sp_onehot = lc->sp.as<uint32_t>();
+        pl.sp_payload = lc->sp.as<uint32_t>() + (size_t)50 * lc->S;
+        pl.rootsum = lc->rootsum.as<uint32_t>();
+    }
     // Every level plane (child seeds, frontier payloads, proof / payload-
     // difference ring, out shares, staged last-level payloads) is written
     // before it is read: level l reads only level l-1's nodes / expanded
@@ -649,7 +658,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
                        rep->nonces.as<uint8_t>() + 16 * base, rep->pub.as<uint8_t>() + ps * base, ins + is * base,
                        hit ? t->L - 1 : 0, t->L + 1);  // a hit recomputes level L-1's payloads: its CW
-    hipLaunchKernelGGL(k_setup, dim3((stride + 255) / 256), dim3(256), 0, c->stream, pl, pfx);
+    hipLaunchKernelGGL(k_setup, dim3((stride + 255) / 256), dim3(256), 0, c->stream, pl, pfx, hit ? 0 : 1);
     HIPCHK(c, hipGetLastError());
 
     const int groups = (n + 63) / 64;  // report groups (rows beyond n are padding)
@@ -721,21 +730,23 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                                    hipMemcpyDeviceToDevice, tail));
         return 0;
     };
-    if (hit) {
+    if (hit && !direct) {
         // levels 0..L-1 from the cache.  The binder messages are BFS-ordered
         // (mastic.py:263-275), so the cached call's message is a prefix of
         // this one's: both sponges resume from their states at the end of the
         // cached call (mid-block, unpadded; k_finalize pads a register copy).
         if (from_cache(pl.sp_onehot, lc->sp.as<uint32_t>(), 50)) return -1;
         if (from_cache(pl.sp_payload, lc->sp.as<uint32_t>() + (size_t)50 * lc->S, 50)) return -1;
+        // the root sum of the cached level-0 evaluation (counter check)
+        if (from_cache(pl.rootsum, lc->rootsum.as<uint32_t>(), (size_t)wlw)) return -1;
+    }
+    if (hit) {
         // (no timing events for the cached levels: nothing is launched for
         // them, and 6 records per level cost ~1.4 ms of host time at L = 255)
         for (int lv = 0; lv < t->L; lv++) {
             f_oh = (f_oh + 2 * t->n_parents[lv] * 32) % KECCAK_RATE;
             f_pl = (f_pl + (lv > 0 ? t->n_parents[lv] * wlw * 4 : 0)) % KECCAK_RATE;
         }
-        // the root sum of the cached level-0 evaluation (counter check)
-        if (from_cache(pl.rootsum, lc->rootsum.as<uint32_t>(), (size_t)wlw)) return -1;
     }
     // the last level's node proofs in the level kernel (after each workgroup's
     // parents) instead of a k_node_proof launch: cache hits, and with
@@ -764,7 +775,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.in_stride = hit ? (int)lc->S : stride;
         a.fr_w_out = plane(wl.fr_w[l & 1]);
         a.payload = pay_buf(l);
-        a.out = plane(wl.out);
+        a.out = R.out.as<uint32_t>() + base;  // columns base .. base + n of the result planes
+        a.out_stride = (int)R.stride;
         a.force_slow_blk = c->force_slow_blk;
         // frontier cache: stage this level's convert seeds (last level); on a
         // hit recompute the parents' payloads from the cached ones into the
@@ -882,7 +894,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                            flp_consts<F>(p));
     }
     HIPCHK(c, hipGetLastError());
-    if (lc) {
+    if (lc && !direct) {
         // frontier cache for the next level (the last level's nodes are in the
         // spare slot already, written by its level kernel): the root sum
         if (!hit && to_cache(lc->rootsum.as<uint32_t>(), pl.rootsum, (size_t)wlw)) return -1;
@@ -890,13 +902,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         if (to_cache(lc->sp.as<uint32_t>(), pl.sp_onehot, 50)) return -1;
         if (to_cache(lc->sp.as<uint32_t>() + (size_t)50 * lc->S, pl.sp_payload, 50)) return -1;
     }
-    // results -> the agg_id slot (plane stride = all reports)
-    Result& R = c->res[agg_id];
+    // results -> the agg_id slot (plane stride = all reports; the level
+    // kernel wrote the out shares there)
     int rc = 0;
     rc |= copy_planes(c, R.eval_proof, R.stride, base, pl.eval_proof, stride, n, 8, tail);
     rc |= copy_planes(c, R.status, R.stride, base, (const uint32_t*)pl.status, stride, n, 1, tail);
-    rc |= copy_planes(c, R.out, R.stride, base, plane(wl.out), stride, n,
-                      (size_t)t->n_prefixes * (1 + p.output_len) * p.w32, tail);
     if (t->weight_check) {
         rc |= copy_planes(c, R.verifier, R.stride, base, pl.verifier, stride, n, (size_t)p.verifier_len * p.w32,
                           tail);

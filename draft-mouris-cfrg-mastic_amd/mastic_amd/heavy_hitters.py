@@ -59,20 +59,39 @@ def _child_packed(packed: bytes, level: int, bit: bool) -> bytes:
 def _unshard_raw(mastic: Mastic, raw_shares, num_measurements):
     """``mastic.unshard`` (mastic.py:399-411) on encode_vec agg shares (the
     two aggregators', or one already-merged total), summed as integers mod p
-    (same result, without a field object per share element)."""
+    (same result, without a field object per share element; Field64 in
+    numpy: 2^64 = 2^32 - 1 mod p)."""
     f = mastic.field
     enc = f.ENCODED_SIZE
+    p = f.MODULUS
+    k = 1 + mastic.OUTPUT_LEN
     if enc == 8:
-        vecs = [np.frombuffer(r, dtype="<u8").tolist() for r in raw_shares]
+        acc = None
+        for r in raw_shares:
+            v = np.frombuffer(r, dtype="<u8")
+            if v.size and int(v.max()) >= p:
+                raise ValueError("encoded element out of range")
+            if acc is None:
+                acc = v.copy()
+                continue
+            t = acc + v  # wraps mod 2^64
+            t += (t < acc).astype(np.uint64) * np.uint64(0xFFFFFFFF)
+            acc = np.where(t >= np.uint64(p), t - np.uint64(p), t)
+        ints = [] if acc is None else acc.tolist()
     else:
         vecs = [[int.from_bytes(r[i:i + enc], "little") for i in range(0, len(r), enc)] for r in raw_shares]
-    p = f.MODULUS
-    for v in vecs:
-        if v and max(v) >= p:
-            raise ValueError("encoded element out of range")
-    agg = [f(sum(col) % p) for col in zip(*vecs)]
-    k = 1 + mastic.OUTPUT_LEN
-    return [mastic.decode_result(agg[i + 1:i + k], agg[i].int()) for i in range(0, len(agg), k)]
+        for v in vecs:
+            if v and max(v) >= p:
+                raise ValueError("encoded element out of range")
+        ints = [sum(col) % p for col in zip(*vecs)]
+    if mastic.circuit in ("Count", "Sum"):  # Mastic.decode_result: the one output element
+        return ints[1::k]
+    return [ints[i + 1:i + k] for i in range(0, len(ints), k)]
+
+
+def _unpack_prefix(packed: bytes, length: int):
+    """The tuple of bools of an MSB-first packed prefix (vidpf.py:33-39)."""
+    return tuple(bool((packed[i // 8] >> (7 - i % 8)) & 1) for i in range(length))
 
 
 def joint_rand_confirmed(msgs: bytes, jr_seeds_0: bytes, jr_seeds_1: bytes, n: int):
@@ -144,16 +163,25 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     prefixes = [(False,), (True,)]
     fast = isinstance(mastic, Mastic)
     packed = [b"\x00", b"\x80"]  # MSB-first packings of ``prefixes`` (fast path)
+    # lazy: the candidates only as packings (no bool tuples per level) when
+    # nothing asks for the tuples: no trace, one default threshold, and no
+    # merge that needs the level's candidates or field-object shares
+    lazy = (fast and trace is None and len(thresholds) == 1
+            and (merge is None or (hasattr(merge, "total") and not hasattr(merge, "begin_level"))))
+    if lazy:
+        prefixes = None
+        th = thresholds['default']
     prev_agg_params = []
     heavy_hitters = []
     bits = mastic.vidpf.BITS
     for level in range(bits):
-        agg_param = (level, tuple(prefixes), level == 0)
+        n_cand = len(packed) if lazy else len(prefixes)
+        agg_param = (level, () if lazy else tuple(prefixes), level == 0)
         assert mastic.is_valid(agg_param, prev_agg_params)
         # encoded once per level (the batch calls take the bytes); the fast
         # path extends the parents' packings instead of re-packing every bit
         if fast:
-            enc = (level.to_bytes(2, "big") + len(prefixes).to_bytes(4, "big") + b"".join(packed)
+            enc = (level.to_bytes(2, "big") + n_cand.to_bytes(4, "big") + b"".join(packed)
                    + bytes([int(level == 0)]))
         else:
             enc = mastic.encode_agg_param(agg_param)
@@ -161,10 +189,10 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
         device_merge = fast and merge is not None and hasattr(merge, "total")
         if merge is not None and hasattr(merge, "begin_level"):
             merge.begin_level(level, prefixes)  # merges that need the level's candidates
-        n_elems = len(prefixes) * (1 + mastic.OUTPUT_LEN) if device_merge else 0
+        n_elems = n_cand * (1 + mastic.OUTPUT_LEN) if device_merge else 0
         raw = agg_shares = None
         tp = time.perf_counter() if phase_times is not None else 0.0
-        if n and prefixes:
+        if n and n_cand:
             # both aggregators' prep_init are queued before either result is
             # fetched, so the host work of the second overlaps the GPU run of
             # the first (stream-ordered; results and timings are per agg_id)
@@ -219,7 +247,18 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
         if trace is not None:
             trace.append(SweepLevel(level, list(prefixes), agg_result, int(alive.sum())))
 
-        if level < bits - 1:
+        if lazy:
+            if level < bits - 1:
+                next_packed = []
+                for (pk, count) in zip(packed, agg_result):
+                    if count >= th:
+                        next_packed.append(_child_packed(pk, level + 1, False))
+                        next_packed.append(_child_packed(pk, level + 1, True))
+                packed = next_packed
+                clock("unshard_prune", tp)
+            else:
+                heavy_hitters = [_unpack_prefix(pk, bits) for (pk, count) in zip(packed, agg_result) if count >= th]
+        elif level < bits - 1:
             next_prefixes = []
             next_packed = []
             for (i, (prefix, count)) in enumerate(zip(prefixes, agg_result)):

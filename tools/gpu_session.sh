@@ -3,6 +3,7 @@
 #   tools/gpu_session.sh <tag> <step> [<step> ...]
 # Steps (each under its own time limit; a fault, abort or timeout ends the script):
 #   tests            pytest -m gpu (verbose log)
+#   ptest:<file>     pytest -m gpu of one test file
 #   smoke            __graft_entry__.smoke()
 #   bench[:cfg[:args]]   bench.py --config cfg (args: extra bench flags, '+' for spaces)
 #   stats[:cfg[:args]]   rocprofv3 --kernel-trace --stats of the same bench
@@ -29,6 +30,7 @@ for s in "$@"; do
     args=${args//+/ }; cfg=${cfg:-c2}
     case $kind in
         tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=15 ;;
+        ptest) step "ptest_$(basename "$cfg" .py)" 600 python -u -m pytest "$cfg" -m gpu -x -v --timeout 120 --timeout-method thread ;;
         smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step "bench_${cfg}" 900 python3 -u bench.py --config "$cfg" $args ;;
         stats) step "stats_${cfg}" 900 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args ;;
