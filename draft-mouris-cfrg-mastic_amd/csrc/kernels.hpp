@@ -684,7 +684,14 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
 #ifndef EVAL_MIN_WAVES
 #define EVAL_MIN_WAVES 5
 #endif
-#define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(EVAL_MIN_WAVES)))
+// The frontier-cache instantiation (FC: a cache hit's one level, a cache-on
+// call's last level) runs with no binder-sponge waves beside it on a hit, so
+// it may take all 128 VGPRs of its 4 waves per SIMD (the LDS-resident tables
+// allow one workgroup per CU): no spills of the recompute / fused-proof state.
+#ifndef EVAL_FC_MIN_WAVES
+#define EVAL_FC_MIN_WAVES 4
+#endif
+#define EVAL_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(FC ? EVAL_FC_MIN_WAVES : EVAL_MIN_WAVES)))
 // workgroup sync words after the key schedules: [0] parent-run counter, [1]
 // node-proof counter (frontier-cache hits), [8, 40) "child seeds stored" bitmap
 // of the workgroup's parents (<= 16 waves x 64 parents per wave)
