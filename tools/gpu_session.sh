@@ -38,7 +38,10 @@ for s in "$@"; do
             step "pmc_sq1_${cfg}" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/sq1_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args
             step "pmc_sq2_${cfg}" 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE -d "$OUT/sq2_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args
             step "pmc_fetch_${cfg}" 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args
-            step "pmc_write_${cfg}" 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args ;;
+            step "pmc_write_${cfg}" 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args
+            # per-kernel summary; the raw per-dispatch CSVs of a sweep exceed gpurun's 64 MiB copy-back
+            python3 tools/pmc_summary.py "$OUT" "_$cfg" > "$OUT/pmc_summary_$cfg.json"
+            rm -rf "$OUT/sq1_$cfg" "$OUT/sq2_$cfg" "$OUT/fetch_$cfg" "$OUT/write_$cfg" ;;
         py) step "py_$(basename "$cfg" .py)" 600 python3 -u "$cfg" $args ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -18,7 +18,8 @@ def load(path):
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in rows:
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        k = k.split("<")[0] + ("<F128>" if "F128" in k else "<F64>" if "F64" in k else "")
+        fc = ",FC" if "true, true" in k else ""  # the frontier-cache instantiation (hits, a cache-on last level)
+        k = k.split("<")[0] + ("<F128%s>" % fc if "F128" in k else "<F64%s>" % fc if "F64" in k else "")
         if r["Dispatch_Id"] not in seen:
             seen.add(r["Dispatch_Id"])
             dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
@@ -27,7 +28,8 @@ def load(path):
     return dur, n, vals
 
 
-def main(d, suffix="", kernels=("k_eval_aes<F64>", "k_eval_aes<F128>", "k_node_proof", "k_absorb_pair", "k_absorb")):
+def main(d, suffix="", kernels=("k_eval_aes<F64>", "k_eval_aes<F128>", "k_eval_aes<F64,FC>", "k_eval_aes<F128,FC>",
+                                 "k_node_proof", "k_absorb_pair", "k_absorb", "k_fold<F64>", "k_fold<F128>")):
     """d: the output directory; suffix: "_<cfg>" for tools/gpu_session.sh pmc:<cfg> passes."""
     out = {}
     dur, n, sq1 = load(os.path.join(d, "sq1%s/run_counter_collection.csv" % suffix))
