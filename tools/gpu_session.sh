@@ -32,7 +32,7 @@ for s in "$@"; do
         tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=15 ;;
         ptest) step "ptest_$(basename "$cfg" .py)" 600 python -u -m pytest "$cfg" -m gpu -x -v --timeout 120 --timeout-method thread ;;
         smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
-        bench) step "bench_${cfg}" 900 python3 -u bench.py --config "$cfg" $args ;;
+        bench) tag=$(echo "$args" | tr -cd 'a-z0-9'); step "bench_${cfg}${tag:+_$tag}" 900 python3 -u bench.py --config "$cfg" $args ;;
         stats) step "stats_${cfg}" 900 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args ;;
         pmc)
             step "pmc_sq1_${cfg}" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/sq1_$cfg" -o run --output-format csv -- python3 bench.py --config "$cfg" --cpu-baseline 0 $args
