@@ -1291,7 +1291,16 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
 // words 2i + h.  Block word j = alignbit(w[j+1], w[j], amt) as above; lane h
 // needs the j = 2i + h, i.e. stream words base + h + k, k < 42, which it loads
 // itself (the plane offset h*S is part of its per-lane buffer offset).
-__global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
+// Each lane keeps only its own stream words of a block, 2i + h (22 words):
+// the word after each, 2i + h + 1, is the partner lane's word i (h = 0) or
+// i + 1 (h = 1), fetched with one DPP swap per word when the fill offset is not
+// a multiple of 4 (shifted byte image).  22 VGPRs of block buffer instead of
+// 42, so the kernel fits 5 waves per SIMD without spills.
+#ifndef ABSORB_MIN_WAVES
+#define ABSORB_MIN_WAVES 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ABSORB_MIN_WAVES)))
+void k_absorb_pair(Planes pl, AbsorbArgs a) {
     absorb_setprio(a.prio);
     // (launched with optional dynamic LDS that is never touched: it only caps
     // how many absorb workgroups share a CU, see mastic_ctx::absorb_lds)
@@ -1308,6 +1317,7 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     const uint32_t lt = (uint32_t)(r & 63) * 4u;                            // lane offset in a tile row
     const uint32_t rowb = (uint32_t)a.rstride * 4u;                          // bytes between stream words
     const uint32_t lth = lt + (uint32_t)h * rowb;                           // ... of the next word for h = 1
+    const uint32_t rowb2 = 2u * rowb;                                        // own words are every other word
     KHalf s;
 #pragma unroll
     for (int i = 0; i < 25; i++) s.a[i] = pld(sp + (size_t)(2 * i) * S, lbh);
@@ -1318,36 +1328,33 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
     const int amt = (32 - 8 * sh) & 31;
     const int nw = (nb + 3) >> 2;
     const int end = f + nb;
-    constexpr int NL = KECCAK_RATE_WORDS;  // words loaded per lane and block
+    constexpr int NL = KECCAK_RATE_WORDS / 2 + 1;  // words loaded per lane and block: base + 2k + h, k < 22
     auto load_block = [&](int b, uint32_t* w) {
         const int base = KECCAK_RATE_WORDS * b - q - off;
-        if (base >= 0 && base + KECCAK_RATE_WORDS < nw) {
+        if (base >= 0 && base + KECCAK_RATE_WORDS + 1 < nw) {
             const __amdgpu_buffer_rsrc_t rs = mh_rsrc(seg + (size_t)base * a.rstride);
             uint32_t so = 0;  // running opaque row offset, as in k_absorb
 #pragma unroll
             for (int k = 0; k < NL; k++) {
                 w[k] = pld_so(rs, lth, so);
-                so += rowb;
+                so += rowb2;
                 asm volatile("" : "+s"(so));
             }
         } else {
-            // first / last block of the launch: uniform clamped loads of
-            // words base .. base + 42, zero outside [0, nw), then lane h
-            // keeps words h .. h + 41
-            uint32_t t[NL + 1];
+            // first / last block of the launch: clamped loads, zero outside
+            // [0, nw); the word index is per lane (h), so it goes into the
+            // lane offset (the descriptor, from a pointer, must be uniform)
 #pragma unroll
-            for (int k = 0; k < NL + 1; k++) {
-                const int m = base + k;
+            for (int k = 0; k < NL; k++) {
+                const int m = base + 2 * k + h;
                 const int mc = m < 0 ? 0 : (m >= nw ? nw - 1 : m);
-                t[k] = pld(seg + (size_t)mc * a.rstride, lt);
+                w[k] = pld(seg, (uint32_t)mc * rowb + lt);
             }
 #pragma unroll
-            for (int k = 0; k < NL + 1; k++) {
-                const int m = base + k;
-                t[k] = (m >= 0 && m < nw) ? t[k] : 0u;
+            for (int k = 0; k < NL; k++) {
+                const int m = base + 2 * k + h;
+                w[k] = (m >= 0 && m < nw) ? w[k] : 0u;
             }
-#pragma unroll
-            for (int k = 0; k < NL; k++) w[k] = h ? t[k + 1] : t[k];
         }
     };
     // One block buffer.  Per block: XOR the current block (waits for its
@@ -1367,7 +1374,15 @@ __global__ __launch_bounds__(256) void k_absorb_pair(Planes pl, AbsorbArgs a) {
         const bool full = end >= KECCAK_RATE * (b + 1);
         const bool more = end > KECCAK_RATE * (b + 1);
 #pragma unroll
-        for (int i = 0; i < 21; i++) s.a[i] ^= __builtin_amdgcn_alignbit(cur[2 * i + 1], cur[2 * i], amt);
+        for (int i = 0; i < 21; i++) {
+            // stream word 2i + h + 1: the partner's word i (h = 0) or i + 1 (h = 1)
+            uint32_t nxt = 0u;
+            if (sh) {
+                const uint32_t x0 = pair_swap(cur[i]), x1 = pair_swap(cur[i + 1]);
+                nxt = h ? x1 : x0;
+            }
+            s.a[i] ^= __builtin_amdgcn_alignbit(nxt, cur[i], amt);
+        }
         if (!full) break;
         asm volatile("" ::: "memory");
         if (more && a.dbg != 1 && a.dbg != 4) load_block(b + 1, cur);
