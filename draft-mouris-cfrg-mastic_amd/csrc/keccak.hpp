@@ -36,7 +36,12 @@ MH_D u32x2 chi1(u32x2 a, u32x2 b, u32x2 c) {
 // U = rounds per loop iteration (12 = fully unrolled).  Measured on MI355X:
 // rolling the rounds (U = 2) made the binder sponge chain 25 % slower and did
 // not speed up the level kernels beside it, so every caller unrolls fully.
-template <int U = 12>
+// FUSE_D: theta's D[x] = C[x-1] ^ rotl(C[x+1], 1) is never formed, each word
+// takes both terms in one 3-input XOR per half (10 fewer XORs per round); it
+// keeps C live through rho, so the 96-VGPR plain level kernel (whose proof
+// waves run this permutation) uses the unfused form: there it doubled the
+// spills and cost C2 1.6 % (profiles/r04_v17_ab_theta_fusion.txt).
+template <int U = 12, bool FUSE_D = true>
 MH_D void keccak_p12(KState& s) {
     static constexpr uint32_t RCL[12] = {0x8000808bu, 0x0000008bu, 0x00008089u, 0x00008003u,
                                          0x00008002u, 0x00000080u, 0x0000800au, 0x8000000au,
@@ -53,14 +58,24 @@ MH_D void keccak_p12(KState& s) {
             u32x2 t = xor3_64(A[x], A[x + 5], A[x + 10]);
             C[x] = xor3_64(t, A[x + 15], A[x + 20]);
         }
-#pragma unroll
-        for (int x = 0; x < 5; x++) D[x] = xor64(C[(x + 4) % 5], rotl64(C[(x + 1) % 5], 1));
         u32x2 B[25];
+        if constexpr (FUSE_D) {
 #pragma unroll
-        for (int x = 0; x < 5; x++)
+            for (int x = 0; x < 5; x++) D[x] = rotl64(C[(x + 1) % 5], 1);
 #pragma unroll
-            for (int y = 0; y < 5; y++)
-                B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(xor64(A[x + 5 * y], D[x]), KR(x, y));
+            for (int x = 0; x < 5; x++)
+#pragma unroll
+                for (int y = 0; y < 5; y++)
+                    B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(xor3_64(A[x + 5 * y], C[(x + 4) % 5], D[x]), KR(x, y));
+        } else {
+#pragma unroll
+            for (int x = 0; x < 5; x++) D[x] = xor64(C[(x + 4) % 5], rotl64(C[(x + 1) % 5], 1));
+#pragma unroll
+            for (int x = 0; x < 5; x++)
+#pragma unroll
+                for (int y = 0; y < 5; y++)
+                    B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(xor64(A[x + 5 * y], D[x]), KR(x, y));
+        }
 #pragma unroll
         for (int y = 0; y < 5; y++)
 #pragma unroll
@@ -110,12 +125,13 @@ MH_D void keccak_p12_pair(KHalf& s, bool hi) {
 #pragma unroll
         for (int x = 0; x < 5; x++) C[x] = xor3_u32(xor3_u32(A[x], A[x + 5], A[x + 10]), A[x + 15], A[x + 20]);
 #pragma unroll
-        for (int x = 0; x < 5; x++) D[x] = C[(x + 4) % 5] ^ pair_rotl(C[(x + 1) % 5], 1);
+        for (int x = 0; x < 5; x++) D[x] = pair_rotl(C[(x + 1) % 5], 1);  // (C[x-1] folded in below)
         uint32_t B[25];
 #pragma unroll
         for (int x = 0; x < 5; x++)
 #pragma unroll
-            for (int y = 0; y < 5; y++) B[y + 5 * ((2 * x + 3 * y) % 5)] = pair_rotl(A[x + 5 * y] ^ D[x], KR(x, y));
+            for (int y = 0; y < 5; y++)
+                B[y + 5 * ((2 * x + 3 * y) % 5)] = pair_rotl(xor3_u32(A[x + 5 * y], C[(x + 4) % 5], D[x]), KR(x, y));
 #pragma unroll
         for (int y = 0; y < 5; y++)
 #pragma unroll

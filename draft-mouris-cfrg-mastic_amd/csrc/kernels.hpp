@@ -450,7 +450,7 @@ MH_D void np_xor_overflow(KState& s, const uint32_t* x) {
 // position f) and the body  seed || le16(BITS) || le16(level) || path,
 // XORed with the level's proof correction word when the node's control bit
 // t is set.  Writes 8 words through `put(j, w)`.  All positions uniform.
-template <class Put>
+template <bool FUSE_D = true, class Put>
 MH_D void node_proof_one(const PrefixState* np, int f, int bits, int level, int path_bytes, const uint32_t seed[4],
                          const uint32_t* path, uint32_t t, const uint32_t pcw[8], Put put) {
     const int q = f >> 2;
@@ -483,7 +483,7 @@ MH_D void node_proof_one(const PrefixState* np, int f, int bits, int level, int 
 #undef NP_W
     }
     if (cross) {
-        keccak_p12(s);
+        keccak_p12<12, FUSE_D>(s);
         switch (q) {
 #define NP_O(Q) case Q: np_xor_overflow<Q>(s, x); break;
             NP_CASES(NP_O)
@@ -491,7 +491,7 @@ MH_D void node_proof_one(const PrefixState* np, int f, int bits, int level, int 
         }
     }
     s.a[20].hi ^= 0x80000000u;
-    keccak_p12(s);
+    keccak_p12<12, FUSE_D>(s);
 #pragma unroll
     for (int j = 0; j < 8; j++) put(j, kword(s, j) ^ (t ? pcw[j] : 0u));
 }
@@ -763,7 +763,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_in + ((size_t)node * 5 + i) * S_in, lb);
             const uint32_t t = pld(a.cs_in + ((size_t)node * 5 + 4) * S_in, lb);
-            node_proof_one(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
+            node_proof_one<FC>(a.np, a.np_f, p.bits, pl_, a.pv_path_bytes, sd, a.pv_child_path + node * 8, t, pcw,
                            [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
         }
         if (a.proof_prio) __builtin_amdgcn_s_setprio(0);
@@ -812,7 +812,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; i++) sd[i] = pld(a.cs_out + ((size_t)node * 5 + i) * S, lb);
         const uint32_t t = pld(a.cs_out + ((size_t)node * 5 + 4) * S, lb);
-        node_proof_one(a.np, a.np_f, p.bits, l, a.cur_path_bytes, sd, a.cur_child_path + node * 8, t, pcw,
+        node_proof_one<FC>(a.np, a.np_f, p.bits, l, a.cur_path_bytes, sd, a.cur_child_path + node * 8, t, pcw,
                        [&](int j, uint32_t w) { pst(ohg + ((size_t)node * 8 + j) * a.bin_rstride, lt, w); });
     };
     if (a.dbg_skip & 2) goto aes_done;
