@@ -211,6 +211,8 @@ struct mastic_ctx {
         return hipStreamSynchronize(stream) == hipSuccess && hipStreamSynchronize(stream2) == hipSuccess &&
                hipStreamSynchronize(stream3) == hipSuccess;
     }
+    bool fuse_last_miss = false;    // any miss's last level with fused, overlapped node proofs (MASTIC_FUSE_LAST_MISS=1)
+    bool fuse_last_miss_fc = true;  // ... a cache-on miss's (MASTIC_FUSE_LAST_MISS_FC=0: k_node_proof)
     bool hit_absorb_main = true;  // a single-chunk hit's sponges on the main stream (MASTIC_HIT_ABSORB_MAIN=0: sponge stream)
     bool fc_all = false;        // A/B only: the frontier-cache kernel variant at every level (MASTIC_FC_ALL=1)
     int fuse_proofs = 1;        // last level's node proofs in the level kernel, overlapped with its AES: 1 on
@@ -668,6 +670,18 @@ static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst
 // parent-payload recompute, 4 + 3 nblk blocks (LDS: 2 x 133 cycles per block
 // at the kernel's ~50 % LDS efficiency).  C3 (Count): 7 of 16, the c2sweep
 // (Sum 255, 9 payload blocks): 3.
+// ... and of a miss's fused last level: per parent also the extend pair and,
+// with no recompute, 3 + 2 nblk AES blocks; the proof waves also take level
+// L-1's node proofs first (2 np[L-1] of them, spread over level L's parents).
+static int miss_proof_waves(const McParams& p, const mastic_ctx* c, int np_prev, int np_last, bool has_prev) {
+    if (c->hit_proof_waves > 0) return c->hit_proof_waves;
+    const int epb = p.field == 64 ? 2 : 1;
+    const int nblk = (p.value_len + epb - 1) / epb;
+    const double proofs = 2.0 + (has_prev ? 2.0 * np_prev / std::max(1, np_last) : 0.0);
+    const double K = 1585.0 * proofs, A = (4.0 + 2.0 * nblk) * 532.0;
+    return std::max(1, std::min(12, (int)std::lround(EVAL_WAVES * K / (K + A))));
+}
+
 static int hit_proof_waves(const McParams& p, const mastic_ctx* c) {
     if (c->hit_proof_waves > 0) return c->hit_proof_waves;
     const int epb = p.field == 64 ? 2 : 1;
@@ -828,7 +842,13 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     // the last level's node proofs in the level kernel (after each workgroup's
     // parents) instead of a k_node_proof launch: cache hits, and with
     // MASTIC_FUSE_PROOFS=2 cache-on misses too (whole parents only)
-    const bool fuse_last = hit ? c->fuse_proofs >= 1 : (lc && c->fuse_proofs == 2);
+    // A miss's last level is fused too when the frontier cache is on (the
+    // sweeps: c2sweep +1 %, its level kernels -4 %), not without it (C2 -1.7 %,
+    // C5 -0.9 %: the FC kernel's 128 VGPRs leave no room for the previous
+    // level's sponge waves beside it; profiles/r04_v21_ab_fused_last_miss.txt)
+    const bool fuse_last = hit ? c->fuse_proofs >= 1
+                               : ((lc && (c->fuse_proofs == 2 || (c->fuse_proofs >= 1 && c->fuse_last_miss_fc))) ||
+                                  (c->fuse_last_miss && c->fuse_proofs >= 1));
     // The last level's sponges: on the main stream for a hit that runs as one
     // chunk (nothing to overlap them with: the next work on the main stream
     // needs them; the cross-stream event round trip cost ~0.08 ms per call),
@@ -873,7 +893,9 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         a.cur_child_path = t->d_path + t->off[l] * 8;
         a.cur_onehot = oh_buf(l);
         a.aes_waves = EVAL_WAVES - c->proof_waves;
-        if (fuse && a.fuse_proofs == 1) a.aes_waves = EVAL_WAVES - hit_proof_waves(p, c);
+        if (fuse && a.fuse_proofs == 1)
+            a.aes_waves = EVAL_WAVES - (hit ? hit_proof_waves(p, c) : miss_proof_waves(p, c, t->n_parents[l - 1 < 0 ? 0 : l - 1],
+                                                                                      np_, l > 0));
         a.par_waves = par_waves;
         a.proof_prio = c->proof_prio;
         a.aes_prio = c->aes_prio;
@@ -901,7 +923,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // payloads recomputed, fused proofs); a miss's other levels run the
         // plain kernel (the variant's uniform branches and extra spills cost
         // a few per cent)
-        if (lc && (hit || l == t->L || c->fc_all))
+        if ((lc && (hit || l == t->L || c->fc_all)) || fuse)
             hipLaunchKernelGGL((k_eval_aes<F, true, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
                                p, pl, a);
         else if (l == 0 || l == t->L)
@@ -1906,6 +1928,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (fa) c->fc_all = fa[0] == '1';
         const char* cr = getenv("MASTIC_CHUNK_REPORTS");
         if (cr) c->chunk_max = (size_t)std::max(0, atoi(cr));
+        const char* flm = getenv("MASTIC_FUSE_LAST_MISS");
+        if (flm) c->fuse_last_miss = flm[0] == '1';
+        const char* flf = getenv("MASTIC_FUSE_LAST_MISS_FC");
+        if (flf) c->fuse_last_miss_fc = flf[0] != '0';
         const char* ham = getenv("MASTIC_HIT_ABSORB_MAIN");
         if (ham) c->hit_absorb_main = ham[0] != '0';
     }
