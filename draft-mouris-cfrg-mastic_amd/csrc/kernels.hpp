@@ -1198,6 +1198,7 @@ struct AbsorbArgs {
     int f[2];
     int prio;  // s_setprio of the sponge waves (0..3)
     int dbg;   // timing experiments only (results wrong): 1 no loads, 2 no permutations, 4 neither (sleeps)
+    int which0;  // sponge of grid row 0 (0 one-hot, 1 payload): a launch covers which0 .. which0 + gridDim.y - 1
 };
 MH_D void absorb_setprio(int prio) {
     switch (prio) {
@@ -1218,7 +1219,7 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
     // level-eval waves: win every issue arbitration on the shared SIMD.
     absorb_setprio(a.prio);
     const int r = blockIdx.x * 256 + threadIdx.x;
-    const int which = blockIdx.y;
+    const int which = a.which0 + (int)blockIdx.y;
     if (r >= pl.stride) return;
     const int nb = a.nbytes[which];
     if (nb == 0) return;
@@ -1306,7 +1307,7 @@ void k_absorb_pair(Planes pl, AbsorbArgs a) {
     // how many absorb workgroups share a CU, see mastic_ctx::absorb_lds)
     const int h = threadIdx.x & 1;
     const int r = blockIdx.x * (int)(blockDim.x >> 1) + (int)(threadIdx.x >> 1);
-    const int which = blockIdx.y;
+    const int which = a.which0 + (int)blockIdx.y;
     if (r >= pl.stride) return;  // both lanes of a pair leave together
     const int nb = a.nbytes[which];
     if (nb == 0) return;

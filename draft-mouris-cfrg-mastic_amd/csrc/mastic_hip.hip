@@ -211,6 +211,7 @@ struct mastic_ctx {
         return hipStreamSynchronize(stream) == hipSuccess && hipStreamSynchronize(stream2) == hipSuccess &&
                hipStreamSynchronize(stream3) == hipSuccess;
     }
+    int split_sponges = -1;  // payload sponge a level earlier, on the third stream: -1 Field128 only, 0 never, 1 always (MASTIC_SPLIT_SPONGES)
     bool fuse_last_miss = false;    // any miss's last level with fused, overlapped node proofs (MASTIC_FUSE_LAST_MISS=1)
     bool fuse_last_miss_fc = true;  // ... a cache-on miss's (MASTIC_FUSE_LAST_MISS_FC=0: k_node_proof)
     bool hit_absorb_main = true;  // a single-chunk hit's sponges on the main stream (MASTIC_HIT_ABSORB_MAIN=0: sponge stream)
@@ -780,8 +781,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     auto pay_buf = [&](int lv) -> uint32_t* { return plane(wl.payload[lv % NSLOT]); };
     auto oh_gs = [&](int) -> int { return oh_gstride; };
     auto pay_gs = [&](int) -> int { return pay_gstride; };
-    auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5, hipStream_t as) -> int {
+    // Sponges which0 .. which0 + nwh - 1 (0 one-hot, 1 payload) of level lv on
+    // stream `as` after `ready`; *done marks their end.
+    auto launch_sponges = [&](int lv, int which0, int nwh, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5,
+                              hipStream_t as, hipEvent_t* done) -> int {
         AbsorbArgs ab;
+        ab.which0 = which0;
         ab.seg[0] = oh_buf(lv);
         ab.gstride[0] = oh_gs(lv);
         ab.nbytes[0] = 2 * t->n_parents[lv] * 32;
@@ -794,22 +799,39 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         ab.prio = c->absorb_prio;
         ab.dbg = c->absorb_dbg;
         if (as != c->stream) HIPCHK(c, hipStreamWaitEvent(as, ready, 0));
-        HIPCHK(c, hipEventRecord(e4, as));
+        if (e4) HIPCHK(c, hipEventRecord(e4, as));
         if (c->dbg_skip & 4) {
             // timing experiments only: no binder sponges (results wrong)
         } else if (c->absorb_pair)
-            hipLaunchKernelGGL(k_absorb_pair, dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, 2),
+            hipLaunchKernelGGL(k_absorb_pair,
+                               dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, (unsigned)nwh),
                                dim3(c->absorb_threads), c->absorb_lds, as, pl, ab);
         else
-            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, 2), dim3(256), 0, as, pl, ab);
-        HIPCHK(c, hipEventRecord(e5, as));
+            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, (unsigned)nwh), dim3(256), 0, as, pl, ab);
+        if (e5) HIPCHK(c, hipEventRecord(e5, as));
         HIPCHK(c, hipGetLastError());
-        abs_done[lv] = get_sync_event(c, sev++);
-        HIPCHK(c, hipEventRecord(abs_done[lv], as));
-        f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
-        f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
+        *done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(*done, as));
+        if (which0 == 0) f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
+        if (which0 + nwh > 1) f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
         return 0;
     };
+    // both sponges of level lv (the default schedule)
+    std::vector<hipEvent_t> pl_done(t->L + 1, nullptr);  // split schedule: payload sponge of each level
+    auto launch_absorb = [&](int lv, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5, hipStream_t as) -> int {
+        return launch_sponges(lv, 0, 2, ready, e4, e5, as, &abs_done[lv]);
+    };
+    // Split schedule (single-chunk misses, MASTIC_SPLIT_SPONGES): level l's
+    // payload differences are complete after eval(l), so its payload sponge
+    // starts then, on the third stream, while its one-hot sponge still waits
+    // for level l's node proofs (eval(l+1)'s proof waves).  The payload chain
+    // -- the long one at C4 / C5 -- then runs a level earlier and leaves a
+    // shorter tail after the last level.
+    // Measured (profiles/r04_v23_ab_split_sponges.txt): C5 +1.4 %, C4 +0.6 %,
+    // C2 -0.5 %, c2sweep -0.9 % -- so by default for Field128 only, whose
+    // payload messages (VALUE_LEN x 16 B per parent) make that chain long.
+    const bool split_on = c->split_sponges < 0 ? p.field == 128 : c->split_sponges > 0;
+    const bool split = split_on && !hit && tail == c->stream && ss == c->stream2;
     // cache planes <-> work planes of this chunk (columns base .. base + n)
     auto from_cache = [&](uint32_t* dst, const uint32_t* src, size_t planes) -> int {
         HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)stride * 4, src + base, lc->S * 4, (size_t)n * 4, planes,
@@ -856,7 +878,10 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const hipStream_t last_as = (hit && tail == c->stream && c->hit_absorb_main) ? c->stream : ss;
     for (int l = hit ? t->L : 0; l <= t->L; l++) {
         const int np_ = t->n_parents[l];
-        if (!hit && l >= NSLOT) HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
+        if (!hit && l >= NSLOT) {
+            HIPCHK(c, hipStreamWaitEvent(c->stream, abs_done[l - NSLOT], 0));
+            if (split && pl_done[l - NSLOT]) HIPCHK(c, hipStreamWaitEvent(c->stream, pl_done[l - NSLOT], 0));
+        }
         AesArgs a;
         a.level = l;
         a.agg_id = agg_id;
@@ -938,7 +963,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipEventRecord(e3, c->stream));
         hipEvent_t aes_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(aes_done, c->stream));
-        if (l > 0 && !hit) {
+        if (split && l > 0) {
+            // payload(l) now, one-hot(l-1) after the proofs this launch made
+            if (launch_sponges(l, 1, 1, aes_done, e4, e5, c->stream3, &pl_done[l])) return -1;
+            if (launch_sponges(l - 1, 0, 1, aes_done, nullptr, nullptr, ss, &abs_done[l - 1])) return -1;
+        } else if (l > 0 && !hit) {
             if (launch_absorb(l - 1, aes_done, e4, e5, ss)) return -1;
         } else {
             HIPCHK(c, hipEventRecord(e4, ss));
@@ -957,7 +986,9 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipEventRecord(e3, c->stream));
         hipEvent_t np_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(np_done, c->stream));
-        if (launch_absorb(l, np_done, e4, e5, last_as)) return -1;
+        if (split ? launch_sponges(l, 0, 1, np_done, e4, e5, last_as, &abs_done[l])
+                  : launch_absorb(l, np_done, e4, e5, last_as))
+            return -1;
     } else {
         // the last level's node proofs, then its sponges
         const int l = t->L;
@@ -986,9 +1017,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipGetLastError());
         hipEvent_t np_done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(np_done, c->stream));
-        if (launch_absorb(l, np_done, e4, e5, last_as)) return -1;
+        if (split ? launch_sponges(l, 0, 1, np_done, e4, e5, last_as, &abs_done[l])
+                  : launch_absorb(l, np_done, e4, e5, last_as))
+            return -1;
     }
     if (tail != last_as) HIPCHK(c, hipStreamWaitEvent(tail, abs_done[t->L], 0));
+    if (split && pl_done[t->L]) HIPCHK(c, hipStreamWaitEvent(tail, pl_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
     hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl, fa, pfx);
     if (t->weight_check) {
@@ -1928,6 +1962,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (fa) c->fc_all = fa[0] == '1';
         const char* cr = getenv("MASTIC_CHUNK_REPORTS");
         if (cr) c->chunk_max = (size_t)std::max(0, atoi(cr));
+        const char* spl = getenv("MASTIC_SPLIT_SPONGES");
+        if (spl) c->split_sponges = spl[0] == '1' ? 1 : 0;
         const char* flm = getenv("MASTIC_FUSE_LAST_MISS");
         if (flm) c->fuse_last_miss = flm[0] == '1';
         const char* flf = getenv("MASTIC_FUSE_LAST_MISS_FC");
