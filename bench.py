@@ -193,33 +193,46 @@ def _oracle_mastic(circuit, kw):
     return om.MasticSumVec(bits, kw["length"], kw["sum_vec_bits"], kw["chunk_length"])
 
 
-def native_cpu_point(m, cfg, enc_ap, reps, vk, ctx, agg_id, threads, n_prefixes, per_thread=2):
+def native_cpu_point(m, cfg, enc_ap, reps, vk, ctx, agg_id, threads, n_prefixes, budget_s=12.0):
     """The native multithreaded CPU baseline (oracle/native_prep.c: AES-NI,
     64-bit Keccak, one thread per report range; the FLP query in the Python
-    oracle): prep_init of per_thread reports per thread of the same workload,
-    timed on the host, its prep shares checked against the GPU's."""
+    oracle): prep_init of the same workload's reports on the host, as many
+    per thread as fill a ~budget_s wall-time sample (one report per thread
+    first, to size it), its prep shares checked against the GPU's.  The
+    value is the C part's rate (VIDPF, binders, eval proof; the FLP query is
+    <1 % of the work and runs in Python here); the rate including the Python
+    FLP is reported beside it."""
     sys.path.insert(0, ROOT)
     from oracle.native import has_aesni, prep_init_native
+    o = _oracle_mastic(cfg["circuit"], cfg["kw"])
+    ap = o.decode_agg_param(enc_ap)
+    psz = m.prep_share_size(ap[2])
+    # calibration: one report per thread (not counted)
+    n1 = min(threads, reps.n)
+    (rn, pub, in0, in1) = reps.view(0, n1).download()
+    t1 = {}
+    prep_init_native(o, vk, ctx, agg_id, ap, rn, pub, in0 if agg_id == 0 else in1, threads, times=t1)
+    per_thread = int(max(2, min(64, budget_s / max(t1["native_c_s"], 1e-3))))
     nn = min(per_thread * threads, reps.n)
     (rn, pub, in0, in1) = reps.view(0, nn).download()
     ins = in0 if agg_id == 0 else in1
-    o = _oracle_mastic(cfg["circuit"], cfg["kw"])
-    ap = o.decode_agg_param(enc_ap)
+    tm = {}
     t = time.perf_counter()
-    (shares, _outs) = prep_init_native(o, vk, ctx, agg_id, ap, rn, pub, ins, threads)
+    (shares, _outs) = prep_init_native(o, vk, ctx, agg_id, ap, rn, pub, ins, threads, times=tm)
     wall = time.perf_counter() - t
     (gps, _js, _o, _st) = m.prep_init_batch(vk, ctx, agg_id, enc_ap, rn, pub, ins, want_out_shares=False)
-    psz = m.prep_share_size(ap[2])
     parity = all(gps[psz * i:psz * (i + 1)] == shares[i] for i in range(nn))
     return {
-        "value": nn * n_prefixes / wall,
+        "value": nn * n_prefixes / tm["native_c_s"],
         "unit": "report*prefix/s",
         "cores": threads,
         "kind": "port",
+        "value_with_python_flp": nn * n_prefixes / wall,
         "impl": "native C (oracle/native_prep.c): AES-NI %s, 64-bit Keccak-p, pthreads; FLP query in the Python "
-                "oracle" % ("on" if has_aesni() else "off (byte-wise AES)"),
-        "sample": "%d reports x %d prefixes on %d threads (%d per thread), %.2f s; GPU/CPU prep shares "
-                  "bit-identical: %s" % (nn, n_prefixes, threads, per_thread, wall, parity),
+                "oracle (timed separately)" % ("on" if has_aesni() else "off (byte-wise AES)"),
+        "sample": "%d reports x %d prefixes on %d threads (%d per thread): C part %.2f s, + Python FLP %.2f s; "
+                  "GPU/CPU prep shares bit-identical: %s" % (nn, n_prefixes, threads, per_thread,
+                                                            tm["native_c_s"], tm["flp_py_s"], parity),
         "parity": parity,
     }
 
@@ -245,6 +258,20 @@ def max_over_ranks(dist, torch, x):
     tt = torch.tensor([x], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
+
+
+def lib_comm_init(m, dist, world, rank):
+    """Join m's ctx to the library's own RCCL communicator: rank 0 creates the
+    id (mastic_comm_unique_id), the gloo control group broadcasts it, every
+    rank calls mastic_comm_init (collective)."""
+    from mastic_amd.merge import exchange_unique_id
+
+    def bcast(obj):
+        box = [obj]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    m.comm_init(world, rank, exchange_unique_id(m, rank, bcast))
 
 
 # ---------------------------------------------------------------- sweeps
@@ -371,7 +398,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     the other ranks' aggregates added in plaintext (VirtualRanksMerge)."""
     from mastic_amd import Mastic
     from mastic_amd.heavy_hitters import compute_heavy_hitters
-    from mastic_amd.merge import merge_field_shares
+    from mastic_amd.merge import CommMerge, merge_field_shares
 
     split = args.split if split is None else split
     steps = args.steps if steps is None else steps
@@ -420,20 +447,41 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     thresholds = {"default": threshold}
     if vr > 1:
         merge = VirtualRanksMerge(m, alphas_job[n_rep:], w_job[n_rep:])
+    elif dist and getattr(args, "lib_comm", False):
+        lib_comm_init(m, dist, world, rank)
+        merge = CommMerge(m)
     else:
         merge = merge_field_shares(m, dist) if dist else None
 
     cached_levels = []
     phases = {}
+    # cpu_parity_cached: the leader prep shares of the CPU leg's sample reports
+    # at its sample levels, as the warmup sweep (frontier cache on, the timed
+    # path) computed them; the CPU leg replays the same reports and levels in
+    # the oracle (spec-literal) and compares
+    procs = cpu_pool_size(args.cpu_procs)
+    check_levels = set(range(0, bits, max(1, bits // 8))[:8])
+    captured = {}
+    want_capture = rank == 0 and world == 1 and do_cpu and warmup > 0
 
-    def step(trace, timing):
+    def capture(level, enc, dev):
+        if level in check_levels:
+            (ps, _js, _o, _st) = m.prep_result(dev, 0, enc)
+            psz = m.prep_share_size(level == 0)
+            captured[level] = [ps[psz * i:psz * (i + 1)] for i in range(min(procs, dev.n))]
+
+    def step(trace, timing, hook=None):
         cached_levels.clear()
         return compute_heavy_hitters(m, ctx, thresholds, reps, verify_key=vk, trace=trace, merge=merge,
                                      timing=timing, frontier_cache=bool(args.frontier_cache),
-                                     cached_levels=cached_levels, phase_times=phases if timing is not None else None)
+                                     cached_levels=cached_levels, phase_times=phases if timing is not None else None,
+                                     level_hook=hook)
 
+    captured_hits = []
     for i in range(warmup):
-        step(None, None)
+        step(None, None, capture if (want_capture and i == 0) else None)
+        if want_capture and i == 0:
+            captured_hits = sorted(set(cached_levels) & set(captured))
         if rank == 0:
             print("[sweep] warmup %d done" % (i + 1), file=sys.stderr, flush=True)
     m.synchronize()
@@ -596,8 +644,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     if rank == 0 and world == 1 and do_cpu:
         # oracle prep_init (leader) of one report per process at 8 levels spread over the sweep,
         # with the GPU trace's candidate prefixes: a bounded sample of the same workload
-        procs = cpu_pool_size(args.cpu_procs)
-        lvls = [lv for lv in traces[0] if lv.prefixes][::max(1, len(traces[0]) // 8)][:8]
+        lvls = [lv for lv in traces[0] if lv.prefixes and lv.level in check_levels]
         (rn, pub, in0, _in1) = reps.view(0, procs).download()
         ps, isz = m.sizes.public_share_size, m.sizes.input_share_size[0]
         spec = (cfg["circuit"], cfg["kw"])
@@ -620,6 +667,17 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             psz = m.prep_share_size(lv.level == 0)
             gpu_ps.append([gps[psz * i:psz * (i + 1)] for i in range(procs)])
         parity = all(res[i * len(lvls) + k][1] == gpu_ps[k][i] for i in range(procs) for k in range(len(lvls)))
+        if captured:
+            # the timed path itself (frontier cache on, sponges resumed from
+            # cached states at the hit levels) against the oracle
+            out["cpu_parity_cached"] = all(
+                lv.level in captured and res[i * len(lvls) + k][1] == captured[lv.level][i]
+                for i in range(procs) for (k, lv) in enumerate(lvls))
+            out["cpu_parity_cached_levels"] = {
+                "levels": [lv.level for lv in lvls], "of_which_frontier_cache_hits": captured_hits,
+                "reports": procs,
+                "what": "leader prep shares of the warmup sweep (frontier cache on) vs the oracle's spec-literal "
+                        "prep_init of the same reports and candidate lists"}
         cu = procs * sum(len(lv.prefixes) for lv in lvls)
         out["cpu_baseline"] = {
             "value": cu / wall,
@@ -635,7 +693,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
         # the native multithreaded CPU point at the same levels (8 reports per thread)
-        nat_t, nat_u, nat_ok = 0.0, 0, True
+        nat_t, nat_u, nat_ok, nat_times = 0.0, 0, True, {}
         nn = min(8 * procs, reps.n)
         (nrn, npub, nin0, _nin1) = reps.view(0, nn).download()
         sys.path.insert(0, ROOT)
@@ -644,7 +702,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         for lv in lvls:
             ap = (lv.level, tuple(lv.prefixes), lv.level == 0)
             t = time.perf_counter()
-            (nsh, _o) = prep_init_native(o, vk, ctx, 0, ap, nrn, npub, nin0, procs)
+            (nsh, _o) = prep_init_native(o, vk, ctx, 0, ap, nrn, npub, nin0, procs, times=nat_times)
             nat_t += time.perf_counter() - t
             nat_u += nn * len(lv.prefixes)
             enc_ap = m.encode_agg_param(ap)
@@ -652,12 +710,14 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             psz = m.prep_share_size(ap[2])
             nat_ok = nat_ok and all(gps[psz * i:psz * (i + 1)] == nsh[i] for i in range(nn))
         out["cpu_baseline"]["native"] = {
-            "value": nat_u / nat_t, "unit": "report*prefix/s", "cores": procs, "kind": "port",
+            "value": nat_u / nat_times["native_c_s"], "unit": "report*prefix/s", "cores": procs, "kind": "port",
+            "value_with_python_flp": nat_u / nat_t,
             "impl": "native C (oracle/native_prep.c): AES-NI %s, 64-bit Keccak-p, pthreads; FLP query in the "
-                    "Python oracle" % ("on" if has_aesni() else "off"),
+                    "Python oracle (timed separately)" % ("on" if has_aesni() else "off"),
             "sample": "%d reports x leader prep_init at levels %s (the sweep's candidate lists) on %d threads, "
-                      "%.2f s; GPU/CPU prep shares bit-identical: %s" % (nn, [lv.level for lv in lvls], procs,
-                                                                           nat_t, nat_ok),
+                      "C part %.2f s (+ Python FLP %.2f s); GPU/CPU prep shares bit-identical: %s" % (
+                          nn, [lv.level for lv in lvls], procs, nat_times["native_c_s"], nat_times["flp_py_s"],
+                          nat_ok),
             "parity": nat_ok,
         }
     del reps
@@ -710,6 +770,12 @@ def cpu_pool_size(requested):
     omp = os.environ.get("OMP_NUM_THREADS")
     if omp and omp.isdigit() and int(omp) > 0:
         n = min(n, int(omp))
+    try:  # cgroup v2 CPU quota
+        (q, period) = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(period))))
+    except (OSError, ValueError):
+        pass
     if requested > 0:
         n = min(n, requested)
     return max(1, n)
@@ -728,8 +794,17 @@ def cpu_host_info():
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = None
+    quota = None
+    try:  # cgroup v2 CPU quota: the CPUs this lease is granted (e.g. "1600000 100000" = 16)
+        (q, period) = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(period)
+    except (OSError, ValueError):
+        pass
     return {"cpu_model": model, "host_cpu_count": os.cpu_count(), "affinity_cpus": aff,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_cpu_quota": quota,
+            "cpu_share_note": "pool = min(affinity, OMP_NUM_THREADS, cgroup quota): the CPUs this lease grants "
+                              "(the GPU box sets OMP_NUM_THREADS to its CPU share; os.cpu_count() counts the "
+                              "whole machine)"}
 
 
 # ---------------------------------------------------------------- main
@@ -747,15 +822,17 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        # MASTIC_BENCH_BACKEND=gloo / MASTIC_BENCH_DEVICE=0: a rehearsal of the
-        # N-rank run with every rank on one GPU (tests); the driver's run is RCCL
+        # The control plane (barriers, the max over ranks, the communicator id)
+        # runs over gloo; the data path's all-gather of agg shares runs on the
+        # library's own RCCL communicator (mastic_comm_init, one per Mastic
+        # ctx).  MASTIC_BENCH_BACKEND=gloo / MASTIC_BENCH_DEVICE=0: a rehearsal
+        # of the N-rank run with every rank on one GPU (tests; RCCL refuses two
+        # ranks on one device), whose shares then move through gloo.
         backend = os.environ.get("MASTIC_BENCH_BACKEND", "nccl")
         local = int(os.environ.get("MASTIC_BENCH_DEVICE", local))
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
+        args.lib_comm = backend == "nccl"
     if args.lib:
         from mastic_amd import _lib
         _lib.load(args.lib)
@@ -763,6 +840,7 @@ def main():
     from mastic_amd.merge import aggregate_to_tensor, fold_on_gpu, merge_agg_shares
 
     cfg = CONFIGS[args.config]
+    lib_comm = getattr(args, "lib_comm", False)
     n_rep = args.reports or cfg["reports"]
     if cfg.get("sweep"):
         run_sweep(args, cfg, world, rank, local, dist, torch)
@@ -786,6 +864,8 @@ def main():
     m = Mastic(bits, cfg["circuit"], device=local, **kw)
     if args.memory_budget_gb:
         m.set_memory_budget(int(args.memory_budget_gb * 2 ** 30))
+    if lib_comm:
+        lib_comm_init(m, dist, world, rank)
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
     # distinct reports resident in HBM: all of them, or a pool the job cycles through
@@ -808,8 +888,11 @@ def main():
 
     def step(reps):
         m.prep_init_device(reps, vk, ctx, args.agg_id, enc_ap)
+        if world > 1 and lib_comm:
+            # agg share folded into HBM, all-gathered over the library's RCCL
+            # communicator and merged mod p on the GPU, in one call
+            return m.aggregate_merged((args.agg_id,), n_elems)
         if world > 1:
-            # agg share folded into HBM, RCCL all-gather, on-GPU mod-p fold
             return merge_agg_shares(m, aggregate_to_tensor(m, args.agg_id, n_elems), dist)
         return m.aggregate_device(args.agg_id, enc_ap, raw=True)
 
@@ -954,7 +1037,11 @@ def main():
                 print("[full_job] %d / %d slices, %.0f s" % (j + 1, len(bounds), t_last - t1), file=sys.stderr,
                       flush=True)
         job = fold_on_gpu(m, torch.cat(parts), len(parts), n_elems)
-        if world > 1:
+        if world > 1 and lib_comm:
+            merged = torch.empty_like(job)
+            m.allgather_fold(job.data_ptr(), 1, n_elems, merged.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            job = merged
+        elif world > 1:
             job = merge_agg_shares(m, job, dist)
         m.synchronize()
         torch.cuda.synchronize()
@@ -973,7 +1060,8 @@ def main():
             "slices": len(bounds),
             "distinct_reports_resident": n_res,
             "what": "prep_init (leader) + fold of every report of the job, %d slices of <= %d, slice agg shares "
-                    "merged mod p on the GPU (mastic_fold_shares)" % (len(bounds), n_rep),
+                    "merged mod p on the GPU (mastic_fold_shares%s)" % (
+                        len(bounds), n_rep, "; ranks' shares: mastic_allgather_fold" if lib_comm else ""),
         }
     out["config"]["resident_reports_per_rank"] = n_res
     (free_b, total_b) = torch.cuda.mem_get_info()
@@ -1060,6 +1148,8 @@ def main():
             out["north_star"]["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind",
                                                                     "single_process_value", "sample")}
             out["north_star"]["cpu_parity"] = ns.get("cpu_parity")
+            out["north_star"]["cpu_parity_cached"] = ns.get("cpu_parity_cached")
+            out["north_star"]["cpu_parity_cached_levels"] = ns.get("cpu_parity_cached_levels")
             # like for like: the CPU leg evaluates whole trees (spec-literal, no
             # cache), so the spec-literal GPU rate is the comparable one; the
             # cached rate's ratio is kept beside it, labelled

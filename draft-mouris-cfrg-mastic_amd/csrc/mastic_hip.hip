@@ -5,6 +5,8 @@
 // the kernels of kernels.hpp / shard.hpp.
 #include "mastic_hip.h"
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -169,6 +171,10 @@ struct mastic_ctx {
     hipStream_t stream3 = nullptr;  // binder sponges of the odd chunks of a pipelined prep_init
     std::vector<hipEvent_t> sync_ev;
     hipEvent_t fold_ev = nullptr;  // mastic_fold_shares: producer stream -> stream
+    // library-owned RCCL communicator (mastic_comm_init; none = world 1)
+    ncclComm_t comm = nullptr;
+    int comm_n = 1, comm_rank = 0;
+    DevBuf comm_local, comm_gather, comm_out;  // mastic_aggregate_merged / mastic_allgather_fold staging
     PrefixState pfx_host[PFX_COUNT];
     std::string err;
     uint64_t budget = 0;
@@ -271,6 +277,7 @@ struct mastic_ctx {
             for (auto e : x.ev) (void)hipEventDestroy(e);
         for (auto e : sync_ev) (void)hipEventDestroy(e);
         if (fold_ev) (void)hipEventDestroy(fold_ev);
+        if (comm) (void)ncclCommDestroy(comm);
         if (tree_ev) (void)hipEventDestroy(tree_ev);
         if (tree_stage) (void)hipHostFree(tree_stage);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1498,8 +1505,8 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     return 0;
 }
 
-extern "C" int mastic_aggregate_device_on_stream(mastic_ctx* c, int agg_id, const uint8_t* valid,
-                                                 void* dev_agg_share, void* caller_stream) {
+extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share,
+                                       void* caller_stream) {
     DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     Result& R = c->res[agg_id];
@@ -1518,9 +1525,10 @@ extern "C" int mastic_aggregate_device_on_stream(mastic_ctx* c, int agg_id, cons
     return 0;
 }
 
-// The round-2 signature (ABI version 3): ordered after the null stream's work.
-extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share) {
-    return mastic_aggregate_device_on_stream(c, agg_id, valid, dev_agg_share, nullptr);
+// ABI-4 name of the same function.
+extern "C" int mastic_aggregate_device_on_stream(mastic_ctx* c, int agg_id, const uint8_t* valid,
+                                                 void* dev_agg_share, void* caller_stream) {
+    return mastic_aggregate_device(c, agg_id, valid, dev_agg_share, caller_stream);
 }
 
 extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t n_shares, size_t n_elems,
@@ -1541,6 +1549,153 @@ extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t 
         hipLaunchKernelGGL(k_fold_shares<F128>, grid, dim3(256), 0, c->stream, (const uint32_t*)dev_shares,
                            (int)n_shares, (int)n_elems, (uint32_t*)dev_out);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---- multi-GPU merge over the ctx's own RCCL communicator --
+
+#define NCCLCHK(c, x)                                                                    \
+    do {                                                                                 \
+        const ncclResult_t r_ = (x);                                                     \
+        if (r_ != ncclSuccess) return fail((c), MASTIC_EHIP, "RCCL: %s", ncclGetErrorString(r_)); \
+    } while (0)
+
+// dev_out = sum mod p of the n_local shares of every rank (n_elems elements
+// each), queued on c->stream: one ncclAllGather of this rank's shares into a
+// rank-ordered buffer, then k_fold_shares over the n_local x nranks shares
+// (RCCL's integer sum is not GF(p) addition).  Without a communicator the
+// local shares are folded directly (world 1).
+static int allgather_fold_impl(mastic_ctx* c, const uint32_t* local, size_t n_local, size_t n_elems, uint32_t* out) {
+    const size_t local_bytes = n_local * n_elems * c->p.w32 * 4;
+    const uint32_t* src = local;
+    size_t n_shares = n_local;
+    if (c->comm && local_bytes) {
+        if (!c->comm_gather.grow(local_bytes * (size_t)c->comm_n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+        NCCLCHK(c, ncclAllGather(local, c->comm_gather.p, local_bytes, ncclUint8, c->comm, c->stream));
+        src = c->comm_gather.as<uint32_t>();
+        n_shares = n_local * (size_t)c->comm_n;
+    }
+    if (n_shares > (size_t)INT32_MAX || n_elems > (size_t)INT32_MAX)
+        return fail(c, MASTIC_EINVAL, "too many shares to fold");
+    const dim3 grid((unsigned)((n_elems + 255) / 256));
+    if (c->p.field == 64)
+        hipLaunchKernelGGL(k_fold_shares<F64>, grid, dim3(256), 0, c->stream, src, (int)n_shares, (int)n_elems, out);
+    else
+        hipLaunchKernelGGL(k_fold_shares<F128>, grid, dim3(256), 0, c->stream, src, (int)n_shares, (int)n_elems, out);
+    HIPCHK(c, hipGetLastError());
+    return 0;
+}
+
+extern "C" int mastic_comm_unique_id(uint8_t id_out[MASTIC_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == MASTIC_COMM_ID_BYTES, "ncclUniqueId size");
+    if (!id_out) return MASTIC_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MASTIC_EHIP;
+    std::memcpy(id_out, &id, sizeof(id));
+    return 0;
+}
+
+extern "C" int mastic_comm_init(mastic_ctx* c, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES]) {
+    DeviceScope ds_(c);
+    if (!c) return MASTIC_EINVAL;
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(c, MASTIC_EINVAL, "invalid communicator rank");
+    if (c->comm) return fail(c, MASTIC_EINVAL, "the ctx already has a communicator");
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    NCCLCHK(c, ncclCommInitRank(&comm, nranks, uid, rank));
+    c->comm = comm;
+    c->comm_n = nranks;
+    c->comm_rank = rank;
+    return 0;
+}
+
+extern "C" int mastic_comm_info(const mastic_ctx* c, int* nranks, int* rank) {
+    if (!c) return MASTIC_EINVAL;
+    if (nranks) *nranks = c->comm_n;
+    if (rank) *rank = c->comm_rank;
+    return 0;
+}
+
+extern "C" int mastic_comm_destroy(mastic_ctx* c) {
+    DeviceScope ds_(c);
+    if (!c) return MASTIC_EINVAL;
+    if (c->comm) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        NCCLCHK(c, ncclCommDestroy(c->comm));
+    }
+    c->comm = nullptr;
+    c->comm_n = 1;
+    c->comm_rank = 0;
+    return 0;
+}
+
+extern "C" int mastic_allgather_fold(mastic_ctx* c, const void* dev_local, size_t n_local, size_t n_elems,
+                                     void* dev_out, void* caller_stream) {
+    DeviceScope ds_(c);
+    if (!c) return MASTIC_EINVAL;
+    if (n_elems && (!dev_out || (n_local && !dev_local))) return fail(c, MASTIC_EINVAL, "null share buffer");
+    if (n_elems == 0) return 0;
+    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->fold_ev, (hipStream_t)caller_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->fold_ev, 0));
+    int rc = allgather_fold_impl(c, (const uint32_t*)dev_local, n_local, n_elems, (uint32_t*)dev_out);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int mastic_merge_host(mastic_ctx* c, const uint8_t* host_local, size_t n_local, size_t n_elems,
+                                 uint8_t* host_out) {
+    DeviceScope ds_(c);
+    if (!c) return MASTIC_EINVAL;
+    if (n_elems && (!host_out || (n_local && !host_local))) return fail(c, MASTIC_EINVAL, "null share buffer");
+    if (n_elems == 0) return 0;
+    const size_t ebytes = (size_t)c->p.w32 * 4;
+    if (!c->comm_local.grow(std::max<size_t>(n_local, 1) * n_elems * ebytes) || !c->comm_out.grow(n_elems * ebytes))
+        return fail(c, MASTIC_ENOMEM, "out of device memory");
+    if (n_local)
+        HIPCHK(c, hipMemcpyAsync(c->comm_local.p, host_local, n_local * n_elems * ebytes, hipMemcpyHostToDevice,
+                                 c->stream));
+    int rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(host_out, c->comm_out.p, n_elems * ebytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int mastic_aggregate_merged(mastic_ctx* c, uint32_t agg_mask, const uint8_t* valid, size_t n_elems,
+                                       uint8_t* agg_out) {
+    DeviceScope ds_(c);
+    if (!c) return MASTIC_EINVAL;
+    const bool zeros = (agg_mask & MASTIC_MERGE_ZEROS) != 0;
+    agg_mask &= ~MASTIC_MERGE_ZEROS;
+    if (agg_mask == 0 || agg_mask > 3) return fail(c, MASTIC_EINVAL, "invalid aggregator mask");
+    if (n_elems && !agg_out) return fail(c, MASTIC_EINVAL, "null agg share buffer");
+    if (n_elems == 0) return 0;
+    const size_t ebytes = (size_t)c->p.w32 * 4;
+    const size_t n_local = (agg_mask & 1) + ((agg_mask >> 1) & 1);
+    if (!c->comm_local.grow(n_local * n_elems * ebytes) || !c->comm_out.grow(n_elems * ebytes))
+        return fail(c, MASTIC_ENOMEM, "out of device memory");
+    size_t k = 0;
+    for (int a = 0; a < 2; a++) {
+        if (!((agg_mask >> a) & 1)) continue;
+        uint32_t* dst = (uint32_t*)((uint8_t*)c->comm_local.p + k++ * n_elems * ebytes);
+        const Result& R = c->res[a];
+        if (!zeros) {
+            if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
+            if ((size_t)R.n_prefixes * (1 + c->p.output_len) != n_elems)
+                return fail(c, MASTIC_EINVAL, "agg share length does not match the last prep_init");
+            int rc = aggregate_impl(c, a, valid, dst);
+            if (rc) return rc;
+        } else {  // this rank holds no reports for the aggregator: agg_init's zeros
+            HIPCHK(c, hipMemsetAsync(dst, 0, n_elems * ebytes, c->stream));
+        }
+    }
+    int rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(agg_out, c->comm_out.p, n_elems * ebytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libmastic_hip.so")
 # The library lib() loads: always the shipped in-tree build, unless an A/B tool
 # calls load(path) explicitly (no process variable can swap it).
 LOAD_PATH = LIB_PATH
-ABI_VERSION = 4  # include/mastic_hip.h MASTIC_ABI_VERSION
+ABI_VERSION = 5  # include/mastic_hip.h MASTIC_ABI_VERSION
 
 MASTIC_OK = 0
 ERRORS = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -5: "EHIP"}
@@ -34,7 +34,11 @@ EXPORTS = [
     "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
     "mastic_aggregate_device", "mastic_reports_view", "mastic_decide_results",
     "mastic_aggregate_device_on_stream", "mastic_abi_version", "mastic_set_test_hooks",
+    "mastic_comm_unique_id", "mastic_comm_init", "mastic_comm_info", "mastic_comm_destroy",
+    "mastic_allgather_fold", "mastic_aggregate_merged", "mastic_merge_host",
 ]
+COMM_ID_BYTES = 128  # MASTIC_COMM_ID_BYTES (= RCCL's NCCL_UNIQUE_ID_BYTES)
+ROCM_PATH = "/opt/rocm"  # librccl.so (the image's ROCm)
 
 
 class MasticParams(ctypes.Structure):
@@ -77,8 +81,10 @@ def build(verbose=False, force=False, out=None, defines=()) -> str:
     if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
         return out
     tmp = out + ".%d.tmp" % os.getpid()
+    rocm_lib = os.path.join(ROCM_PATH, "lib")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I" + INCLUDE] + ["-D" + d for d in defines] + ["-o", tmp, os.path.join(CSRC, "mastic_hip.hip")]
+           "-I" + INCLUDE] + ["-D" + d for d in defines] + ["-o", tmp, os.path.join(CSRC, "mastic_hip.hip"),
+                                                         "-L" + rocm_lib, "-Wl,-rpath," + rocm_lib, "-lrccl"]
     if verbose:
         print(" ".join(cmd))
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -138,7 +144,14 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
                     "mastic_fold_shares": (i32, [P, P, sz, sz, P, P]),
-                    "mastic_aggregate_device": (i32, [P, i32, P, P]),
+                    "mastic_aggregate_device": (i32, [P, i32, P, P, P]),
+                    "mastic_comm_unique_id": (i32, [P]),
+                    "mastic_comm_init": (i32, [P, i32, i32, P]),
+                    "mastic_comm_info": (i32, [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+                    "mastic_comm_destroy": (i32, [P]),
+                    "mastic_allgather_fold": (i32, [P, P, sz, sz, P, P]),
+                    "mastic_aggregate_merged": (i32, [P, ctypes.c_uint32, P, sz, P]),
+                    "mastic_merge_host": (i32, [P, P, sz, sz, P]),
                     "mastic_aggregate_device_on_stream": (i32, [P, i32, P, P, P]),
                     "mastic_abi_version": (i32, []),
                     "mastic_set_test_hooks": (i32, [P, i32, i32]),

@@ -118,7 +118,7 @@ class SweepLevel:
 
 def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verify_key: bytes = None,
                           trace=None, merge=None, timing=None, frontier_cache=None, cached_levels=None,
-                          phase_times=None):
+                          phase_times=None, level_hook=None):
     """poc/examples.py:37-91 on the GPU.
 
     ``reports`` is either the reference's list of
@@ -136,7 +136,9 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
     ``cached_levels`` is a list, the levels that took that path are appended.
     If ``phase_times`` is a dict, the host wall time of each phase of a level
     (enqueueing both prep_inits, decide, aggregate + merge, unshard + prune) is
-    accumulated into it (seconds).
+    accumulated into it (seconds).  ``level_hook(level, enc_agg_param, reports)``
+    (if given) runs after each level's decide, while both aggregators' prep_init
+    results of the level are still in HBM (e.g. to read sampled prep shares).
     """
     def clock(phase, t0):
         if phase_times is not None:
@@ -224,6 +226,8 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                     # prep_next (mastic.py:364-377, called at examples.py:67): each
                     # aggregator's joint-rand seed must equal the prep message
                     alive &= joint_rand_confirmed(msgs, shares[0][1], shares[1][1], n)
+            if level_hook is not None:
+                level_hook(level, enc, dev)
             mask = alive.astype(np.uint8)
             if device_merge:
                 # both shares folded, gathered and merged in HBM (one RCCL call)
@@ -234,6 +238,10 @@ def compute_heavy_hitters(mastic: Mastic, ctx: bytes, thresholds, reports, verif
                 agg_shares = [mastic.aggregate_device(agg_id, enc, mask) for agg_id in range(2)]
         elif device_merge:
             raw = [merge.total(n_elems, have_results=False)]  # same collectives on every rank
+        elif lazy:
+            # no reports: agg_init's zeros for every candidate (the lazy agg
+            # param carries no prefix tuples for agg_init to count)
+            raw = [bytes(n_cand * (1 + mastic.OUTPUT_LEN) * mastic.field.ENCODED_SIZE)]
         else:
             agg_shares = [mastic.agg_init(agg_param) for _ in range(2)]
         tp = clock("aggregate_merge", tp)

@@ -2,19 +2,62 @@
 
 Reports are sharded over ranks (one process per GPU); each rank folds its own
 out shares on its GPU.  The only cross-GPU exchange is the per-prefix
-aggregate share: one all-gather (RCCL over xGMI with the "nccl" backend)
-into a rank-ordered buffer, then a GF(p) sum on the GPU
-(``mastic_fold_shares``) — RCCL's integer sum is not field addition.
-Mirrors ``Mastic.merge`` (poc/mastic.py:390-397).
+aggregate share: one all-gather over xGMI into a rank-ordered buffer, then a
+GF(p) sum on the GPU (``k_fold_shares``) — RCCL's integer sum is not field
+addition.  Mirrors ``Mastic.merge`` (poc/mastic.py:390-397).
 
-The shares stay in HBM from the fold of the out shares
-(``mastic_aggregate_device``) through the all-gather to the GF(p) merge;
-the fold is ordered after the all-gather by an event on the stream RCCL ran
-on (torch's current stream), not by a device-wide synchronisation.
+The product path is :class:`CommMerge`: the library owns the RCCL
+communicator (``mastic_comm_init``) and does fold, all-gather and GF(p) merge
+in HBM in one call (``mastic_aggregate_merged``); no PyTorch is involved, and
+the communicator id crosses processes by whatever channel the caller has
+(:func:`exchange_unique_id` takes any broadcast callable).
+
+The torch forms below (``gather_shares`` / :class:`SweepMerge`) keep the
+same fold and merge kernels but let a ``torch.distributed`` group move the
+shares: a ``gloo`` group is how several ranks share ONE GPU in the one-GPU
+rehearsals (RCCL refuses two ranks on one device).
 """
 import ctypes
 
 from . import _lib
+
+
+def exchange_unique_id(m, rank: int, broadcast):
+    """The communicator id on every rank: rank 0 creates it
+    (``mastic_comm_unique_id``) and ``broadcast(obj_or_None) -> obj`` hands
+    it to the others (e.g. a ``torch.distributed.broadcast_object_list``
+    wrapper, a file or a socket)."""
+    uid = m.comm_unique_id() if rank == 0 else None
+    return bytes(broadcast(uid))
+
+
+class CommMerge:
+    """Per-level merge for the sweep driver over the library's own RCCL
+    communicator.  ``total`` folds both aggregators' out shares on this rank's
+    GPU, all-gathers them across the ranks and sums the 2 x world shares mod p
+    (the collector's ``unshard`` merge, mastic.py:399-411, of the job-wide agg
+    shares), all inside ``mastic_aggregate_merged``; only the final aggregate
+    reaches the host.  Calling the object maps a list of field elements (one
+    aggregator's rank-local agg share) to the job-wide list."""
+
+    def __init__(self, m, nranks: int = None, rank: int = None, unique_id: bytes = None):
+        self.m = m
+        if nranks is not None and m.comm_info()[0] == 1 and nranks > 1:
+            m.comm_init(nranks, rank, unique_id)
+
+    def total(self, n_elems, valid=None, have_results=True) -> bytes:
+        if n_elems == 0:
+            return b""
+        return self.m.aggregate_merged((0, 1), n_elems, None if not have_results else valid,
+                                       zeros=not have_results)
+
+    def __call__(self, agg_share):
+        m = self.m
+        if len(agg_share) == 0:
+            return agg_share
+        raw = bytes(agg_share) if isinstance(agg_share, (bytes, bytearray)) else m.field.encode_vec(agg_share)
+        merged = m.merge_host(raw, 1, len(raw) // m.field.ENCODED_SIZE)
+        return m.field.decode_vec(merged)
 
 
 def _current_stream_handle():
@@ -58,10 +101,10 @@ def aggregate_to_tensor(m, agg_id, n_elems, valid=None, out=None):
     if out is None:
         out = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device="cuda")
     v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-    rc = _lib.lib().mastic_aggregate_device_on_stream(m._ctx, agg_id, _lib.buf(v),
+    rc = _lib.lib().mastic_aggregate_device(m._ctx, agg_id, _lib.buf(v),
                                                       ctypes.c_void_p(out.data_ptr()), _current_stream_handle())
     if rc != 0:
-        raise _lib.MasticError(rc, "mastic_aggregate_device_on_stream failed")
+        raise _lib.MasticError(rc, "mastic_aggregate_device failed")
     return out
 
 

@@ -236,13 +236,75 @@ class Mastic:
         _check(self._ctx, _lib.lib().mastic_prep_result(self._ctx, agg_id, None, None, None, None))
 
     def aggregate_to(self, agg_id: int, valid, dev_ptr: int, stream: int = 0):
-        """``mastic_aggregate_device_on_stream``: fold into caller-owned device memory
+        """``mastic_aggregate_device``: fold into caller-owned device memory
         (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM.
         ``stream`` is the hipStream_t handle whose queued work last touched
         the buffer (0 = the null stream)."""
         v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-        _check(self._ctx, _lib.lib().mastic_aggregate_device_on_stream(
+        _check(self._ctx, _lib.lib().mastic_aggregate_device(
             self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None)))
+
+    # ------------------------------- multi-GPU merge (library-owned RCCL)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """``mastic_comm_unique_id``: rank 0 creates the communicator id and
+        hands it to the other ranks by any channel."""
+        buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+        rc = _lib.lib().mastic_comm_unique_id(buf)
+        if rc != 0:
+            raise _lib.MasticError(rc, "mastic_comm_unique_id failed")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        """``mastic_comm_init``: join this ctx to an RCCL communicator of
+        ``nranks`` GPUs (collective; one process per GPU)."""
+        if len(unique_id) != _lib.COMM_ID_BYTES:
+            raise ValueError("communicator id has incorrect length")
+        _check(self._ctx, _lib.lib().mastic_comm_init(self._ctx, nranks, rank, _lib.buf(bytes(unique_id))))
+
+    def comm_info(self):
+        """(nranks, rank) of the ctx's communicator ((1, 0) without one)."""
+        (n, r) = (ctypes.c_int(), ctypes.c_int())
+        _check(self._ctx, _lib.lib().mastic_comm_info(self._ctx, ctypes.byref(n), ctypes.byref(r)))
+        return (n.value, r.value)
+
+    def comm_destroy(self):
+        _check(self._ctx, _lib.lib().mastic_comm_destroy(self._ctx))
+
+    def allgather_fold(self, dev_local: int, n_local: int, n_elems: int, dev_out: int, stream: int = 0):
+        """``mastic_allgather_fold`` on device pointers: dev_out = the mod-p
+        sum of every rank's n_local shares of n_elems elements."""
+        _check(self._ctx, _lib.lib().mastic_allgather_fold(
+            self._ctx, ctypes.c_void_p(dev_local or None), n_local, n_elems, ctypes.c_void_p(dev_out or None),
+            ctypes.c_void_p(stream or None)))
+
+    def merge_host(self, shares: bytes, n_local: int, n_elems: int) -> bytes:
+        """``mastic_merge_host``: the mod-p sum over the communicator's ranks
+        of n_local encode_vec shares of n_elems elements each (host bytes)."""
+        if len(shares) != n_local * n_elems * self.field.ENCODED_SIZE:
+            raise ValueError("shares have incorrect length")
+        out = np.empty(n_elems * self.field.ENCODED_SIZE, np.uint8)
+        _check(self._ctx, _lib.lib().mastic_merge_host(self._ctx, _lib.buf(bytes(shares)), n_local, n_elems,
+                                                       _lib.buf(out)))
+        return out.tobytes()
+
+    def aggregate_merged(self, agg_ids, n_elems: int, valid=None, zeros=False) -> bytes:
+        """``mastic_aggregate_merged``: the sum over the communicator's ranks
+        (and over ``agg_ids``) of the GPU folds of the last prep_init's out
+        shares, as encode_vec bytes (Mastic.agg_update + merge, mastic.py:384-397).
+        ``zeros``: this rank ran no prep_init and contributes agg_init's
+        zeros (the call is collective)."""
+        mask = 0
+        for a in agg_ids:
+            if a not in (0, 1):
+                raise ValueError("invalid aggregator ID")
+            mask |= 1 << a
+        if zeros:
+            mask |= 4  # MASTIC_MERGE_ZEROS
+        out = np.empty(n_elems * self.field.ENCODED_SIZE, np.uint8)
+        v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
+        _check(self._ctx, _lib.lib().mastic_aggregate_merged(self._ctx, mask, _lib.buf(v), n_elems, _lib.buf(out)))
+        return out.tobytes()
 
     def aggregate_device(self, agg_id: int, agg_param, valid=None, raw=False):
         """Fold the out shares of the last prep_init(_batch) of agg_id on the GPU

@@ -43,8 +43,12 @@ extern "C" {
 #endif
 
 /* ABI version of this header; mastic_abi_version() returns the library's.
- * 4: mastic_aggregate_device_on_stream, mastic_set_test_hooks. */
-#define MASTIC_ABI_VERSION 4
+ * 4: mastic_aggregate_device_on_stream, mastic_set_test_hooks.
+ * 5: mastic_aggregate_device takes the caller's stream again (its round-3,
+ *    pre-versioning signature; ABI 4 had briefly dropped it), the
+ *    library-owned RCCL communicator (mastic_comm_*, mastic_allgather_fold,
+ *    mastic_aggregate_merged). */
+#define MASTIC_ABI_VERSION 5
 
 #define MASTIC_OK 0
 #define MASTIC_EINVAL (-22)
@@ -151,11 +155,12 @@ int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t*
  * leaves HBM.  caller_stream is the hipStream_t whose queued work last
  * touched the buffer (e.g. the stream it was allocated or zero-filled on;
  * NULL = the null stream): the fold is ordered after that work by an event.
- * Returns when the buffer is written.  (ABI 4; the ABI-3 form without a
- * stream, mastic_aggregate_device, orders after the null stream.) */
+ * Returns when the buffer is written.  mastic_aggregate_device_on_stream is
+ * the same function under its ABI-4 name. */
+int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
+                            void* caller_stream);
 int mastic_aggregate_device_on_stream(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
                                       void* caller_stream);
-int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share);
 /* Multi-GPU merge (Mastic.merge, mastic.py:390-397) of n_shares agg shares
  * of n_elems elements each, all in DEVICE memory of the ctx's GPU (e.g. the
  * output of an RCCL all-gather): dev_out[e] = sum_s dev_shares[s][e] mod p.
@@ -165,6 +170,49 @@ int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, v
  * written. */
 int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares, size_t n_elems, void* dev_out,
                        void* producer_stream);
+/* ---- multi-GPU aggregation over a library-owned RCCL communicator ------
+ * One process per GPU, reports split over the ranks.  The
+ * only exchange is the per-prefix agg share: an RCCL all-gather over xGMI,
+ * then the GF(p) fold on the GPU (RCCL's integer sum is not field addition).
+ * Replaces Mastic.merge (mastic.py:390-397) of the ranks' agg shares.
+ * Rank 0 calls mastic_comm_unique_id and hands the id to every rank by any
+ * channel it likes (a file, a socket, a launcher's store); each rank then
+ * calls mastic_comm_init on its ctx (collective: blocks until all nranks
+ * ranks have joined).  A ctx without a communicator behaves as world 1. */
+#define MASTIC_COMM_ID_BYTES 128
+int mastic_comm_unique_id(uint8_t id_out[MASTIC_COMM_ID_BYTES]);
+int mastic_comm_init(mastic_ctx* ctx, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES]);
+/* Number of ranks / this rank of the ctx's communicator (1 / 0 without one). */
+int mastic_comm_info(const mastic_ctx* ctx, int* nranks, int* rank);
+int mastic_comm_destroy(mastic_ctx* ctx);
+/* dev_out[e] = sum over every rank r and local share s of
+ * dev_local_r[s][e] mod p: each rank passes n_local shares of n_elems
+ * elements (encode_vec order) in DEVICE memory, all ranks the same counts.
+ * The all-gather and the fold run on the ctx's stream, ordered after
+ * caller_stream's queued work (NULL = the null stream) by an event.
+ * Collective; returns when dev_out is written. */
+int mastic_allgather_fold(mastic_ctx* ctx, const void* dev_local, size_t n_local, size_t n_elems, void* dev_out,
+                          void* caller_stream);
+/* mastic_allgather_fold on HOST buffers (shares a driver holds in host
+ * memory, e.g. decoded agg shares): host_local n_local x n_elems elements in,
+ * host_out n_elems elements out; staged through the ctx's device buffers.
+ * Collective. */
+int mastic_merge_host(mastic_ctx* ctx, const uint8_t* host_local, size_t n_local, size_t n_elems, uint8_t* host_out);
+/* The whole agg_update + merge of a sharded job in HBM: each selected
+ * aggregator's (agg_mask bit a = agg_id a) out shares of its last prep_init
+ * are folded over the reports with valid[i] != 0 (NULL: all) on this GPU,
+ * all-gathered across the communicator's ranks, and summed mod p; agg_out
+ * (host, n_elems * field_bytes) receives the sum over ranks and over the
+ * selected aggregators.  n_elems = len(prefixes) * (1 + output_len) must
+ * match that prep_init.  A rank that ran no prep_init for this agg param
+ * (no reports on it) adds MASTIC_MERGE_ZEROS and contributes agg_init's
+ * zeros for the selected aggregators.  agg_mask 1 or 2: that aggregator's
+ * job-wide agg share; 3: the collector's merge of both (the heavy-hitters
+ * sweep's per-level total).  Collective: every rank passes the same
+ * aggregators and n_elems. */
+#define MASTIC_MERGE_ZEROS 4u
+int mastic_aggregate_merged(mastic_ctx* ctx, uint32_t agg_mask, const uint8_t* valid, size_t n_elems,
+                            uint8_t* agg_out);
 /* VIDPF-proof aggregation mode (draft-mouris-cfrg-mastic.md, "Plain
  * Heavy-Hitters with VIDPF-Proof Aggregation"; no poc code or wire format in
  * the reference): Merkle tree over the eval proofs of the last prep_init of

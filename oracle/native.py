@@ -66,10 +66,14 @@ def truncation(valid):
 
 
 def prep_init_native(o, verify_key: bytes, ctx: bytes, agg_id: int, agg_param, nonces: bytes, pubs: bytes,
-                     ins: bytes, threads: int):
+                     ins: bytes, threads: int, times=None):
     """prep_init of n reports (wire encodings in) with an oracle Mastic `o`.
     Returns (prep_shares: list of bytes (test_vec_encode_prep_share),
-    out_shares: bytes, n x len(prefixes) x (1 + OUTPUT_LEN) encoded elements)."""
+    out_shares: bytes, n x len(prefixes) x (1 + OUTPUT_LEN) encoded elements).
+    If ``times`` is a dict, the wall seconds of the C part (VIDPF, binders,
+    eval proof: ``native_c_s``) and of the Python FLP part (``flp_py_s``) are
+    added to it."""
+    import time
     (level, prefixes, do_weight_check) = agg_param
     n = len(nonces) // 16
     f = o.field
@@ -94,9 +98,11 @@ def prep_init_native(o, verify_key: bytes, ctx: bytes, agg_id: int, agg_param, n
     ev = ctypes.create_string_buffer(max(32 * n, 1))
     bs = ctypes.create_string_buffer(max(vl * f.ENCODED_SIZE * n, 1))
     out = ctypes.create_string_buffer(max(row * n, 1))
+    t0 = time.perf_counter()
     rc = lib().native_prep_vidpf(8 * f.ENCODED_SIZE, o.vidpf.BITS, vl, agg_id, level, len(prefixes),
                                  bytes(enc_p), tg, tl, darr, dlen, verify_key, len(verify_key), n, nonces, pubs,
                                  psz, ins, isz, threads, ev, bs, out)
+    t1 = time.perf_counter()
     if rc != 0:
         raise ValueError("native_prep_vidpf: bad arguments")
     shares = []
@@ -117,6 +123,9 @@ def prep_init_native(o, verify_key: bytes, ctx: bytes, agg_id: int, agg_param, n
                 joint_rand = o.joint_rand(ctx, o.joint_rand_seed(ctx, parts))
             verifier = o.flp.query(beta_share[1:], proof_share, query_rand, joint_rand, 2)
         shares.append(o.test_vec_encode_prep_share((eval_proof, verifier, jr_part)))
+    if times is not None:
+        times["native_c_s"] = times.get("native_c_s", 0.0) + t1 - t0
+        times["flp_py_s"] = times.get("flp_py_s", 0.0) + time.perf_counter() - t1
     return (shares, out.raw[:row * n])
 
 

@@ -191,3 +191,22 @@ def test_sweep_joint_rand_confirmation_drops_report():
     hh = compute_heavy_hitters(mastic, ctx, {'default': _TotalAtLeast(4)}, dev, verify_key=vk, trace=trace)
     assert all(t.n_valid == len(meas) - 1 for t in trace if t.prefixes)
     assert hh == [index(0b0100, bits), index(0b1011, bits)]
+
+
+@pytest.mark.parametrize("circuit", ["Count", "Histogram"])
+def test_sweep_without_reports_keeps_every_candidate_at_threshold_zero(circuit):
+    """No reports and threshold 0: every candidate's aggregate is agg_init's
+    zero, which reaches the threshold, so every prefix survives every level
+    (examples.py:80-90).  The lazy path (packed candidates, no trace) and the
+    tuple path (with a trace) agree."""
+    from mastic_amd import MasticCount, MasticHistogram
+    from mastic_amd.heavy_hitters import compute_heavy_hitters
+    bits = 3
+    mastic = MasticCount(bits) if circuit == "Count" else MasticHistogram(bits, 3, 2)
+    th = {'default': 0} if circuit == "Count" else {'default': _TotalAtLeast(0)}
+    lazy = compute_heavy_hitters(mastic, b'none', th, [], verify_key=bytes(16))
+    trace = []
+    full = compute_heavy_hitters(mastic, b'none', th, [], verify_key=bytes(16), trace=trace)
+    want = [index(v, bits) for v in range(2 ** bits)]
+    assert lazy == full == want
+    assert [len(t.prefixes) for t in trace] == [2, 4, 8]
