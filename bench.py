@@ -543,6 +543,36 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     dom_ms = sum(t[0] + t[2] for t in timing)
     n_launch = sum(t[1] for t in timing)
     achieved = nodes * dom_ops / (dom_ms / 1e3) / 1e12 if dom_ms > 0 else 0.0
+    # per level of the first timed sweep (both aggregators): where the level
+    # kernel's time goes.  A frontier-cache hit also recomputes each parent's
+    # convert stream (its seed and payload, aes_per_node - 1 blocks) from the
+    # cached convert seed: executed, but not algorithmic work (SURVEY §8d
+    # counts a minimal evaluation), so `frac` leaves it out and
+    # `frac_executed` counts it
+    per_level = {"level": [], "hit": [], "candidates": [], "nodes_per_report": [], "level_kernel_ms": [],
+                 "absorb_ms": [], "frac": []}
+    rec_ops = 0
+    ti = 0
+    for lv in traces[0]:
+        if not lv.prefixes or ti + 1 >= len(timing):
+            continue
+        hit_l = lv.level in hit
+        parents = len(set(p[:lv.level] for p in lv.prefixes)) if lv.level > 0 else 1
+        nl = 2 * parents if hit_l else m.tree_stats((lv.level, tuple(lv.prefixes), lv.level == 0))[0]
+        ms = timing[ti][0] + timing[ti][2] + timing[ti + 1][0] + timing[ti + 1][2]
+        per_level["level"].append(lv.level)
+        per_level["hit"].append(hit_l)
+        per_level["candidates"].append(len(lv.prefixes))
+        per_level["nodes_per_report"].append(nl)
+        per_level["level_kernel_ms"].append(round(ms, 2))
+        per_level["absorb_ms"].append(round(timing[ti][4] + timing[ti + 1][4], 2))
+        per_level["frac"].append(round(2 * n_rep * nl * dom_ops / (ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 3)
+                                 if ms > 0 else None)
+        if hit_l:
+            rec_ops += 2 * n_rep * parents * (aes_per_node - 1) * AES_BLOCK_OPS
+        ti += 2
+    rec_ops *= steps
+    achieved_exec = (nodes * dom_ops + rec_ops) / (dom_ms / 1e3) / 1e12 if dom_ms > 0 else 0.0
     widths = [len(lv.prefixes) for lv in traces[0]]
     if split:
         scaling, workload = "strong", "%s; the job's %d reports split %d-way (%d on this rank)" % (
@@ -596,7 +626,12 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             "launches": n_launch,
             "avg_launch_ms": dom_ms / max(n_launch, 1),
             "ops_per_node": dom_ops,
+            "frac_executed": achieved_exec / VALU_PEAK_TOPS,
+            "frac_executed_note": "also counts the frontier-cache hits' parent convert-stream recompute (%d AES "
+                                  "blocks per parent), which the cache trades for 20 B per cached node" % (
+                                      aes_per_node - 1),
         },
+        "per_level": per_level,
         "breakdown_ms_per_step": {
             "eval_aes_plus_proofs": dom_ms / steps,
             "absorb": sum(t[4] for t in timing) / steps,
@@ -692,13 +727,22 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         }
         out["cpu_baseline"].update(cpu_host_info())
         out["cpu_parity"] = parity
-        # the native multithreaded CPU point at the same levels (8 reports per thread)
-        nat_t, nat_u, nat_ok, nat_times = 0.0, 0, True, {}
-        nn = min(8 * procs, reps.n)
-        (nrn, npub, nin0, _nin1) = reps.view(0, nn).download()
+        # the native multithreaded CPU point at the same levels, on as many
+        # reports as fill a ~10 s sample of its C part (sized from a first
+        # pass over 8 reports per thread, which is not counted)
         sys.path.insert(0, ROOT)
         from oracle.native import has_aesni, prep_init_native
         o = _oracle_mastic(cfg["circuit"], cfg["kw"])
+        nn = min(8 * procs, reps.n)
+        (nrn, npub, nin0, _nin1) = reps.view(0, nn).download()
+        cal = {}
+        for lv in lvls:
+            prep_init_native(o, vk, ctx, 0, (lv.level, tuple(lv.prefixes), lv.level == 0), nrn, npub, nin0, procs,
+                             times=cal)
+        # (capped at 8,192 reports: the level-0 weight check runs the FLP query in Python, ~1 ms each)
+        nn = int(min(reps.n, 8192, max(nn, nn * 10.0 / max(cal["native_c_s"], 1e-3))))
+        (nrn, npub, nin0, _nin1) = reps.view(0, nn).download()
+        nat_t, nat_u, nat_ok, nat_times = 0.0, 0, True, {}
         for lv in lvls:
             ap = (lv.level, tuple(lv.prefixes), lv.level == 0)
             t = time.perf_counter()
@@ -1140,7 +1184,9 @@ def main():
             "heavy_hitters": nc["heavy_hitters"],
             "heavy_hitters_equal_plaintext": nc["heavy_hitters_equal_plaintext"],
             "frac": ns["roofline"]["frac"],
+            "frac_executed": ns["roofline"]["frac_executed"],
             "roofline_kernel": ns["roofline"]["kernel"],
+            "per_level": ns["per_level"],
             "breakdown_ms": ns["breakdown_ms_per_step"],
         }
         if "cpu_baseline" in ns:

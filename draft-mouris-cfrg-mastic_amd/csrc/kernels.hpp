@@ -511,7 +511,17 @@ struct AesArgs {
     int level;
     int agg_id;
     int n_parents;       // parents at this level (1 = the root at level 0)
-    int ppw;             // parents per wave
+    int ppw;             // items per wave (an item is a parent, or one block range of one)
+    // Small levels (few parents: the top of every tree) leave most waves of a
+    // workgroup idle and each parent's ~2 + 2 nblk AES blocks a serial chain
+    // of one wave.  There a parent is split into `split` items: item k
+    // recomputes the parent's extend pair (2 blocks) and evaluates blocks
+    // [k * split_blocks, (k + 1) * split_blocks) of both children's convert
+    // streams (counter mode: the blocks are independent); item 0 also the
+    // next seeds.  Never at a level that emits out shares (the truncation
+    // accumulates across elements) or on a frontier-cache hit.
+    int split;
+    int split_blocks;
     const int32_t* parent_node;  // [n_parents] node index of each parent in level-1 (level >= 1)
     const int32_t* child_exp;    // [2 * n_parents] index into this level's frontier, -1 = leaf
     const int32_t* child_pfx;    // [2 * n_parents] index into the prefix list (level L), -1 = none
@@ -707,7 +717,10 @@ MH_D void parent_payload(const AesPerm& TL, const RkLds& rkc, const uint32_t cv[
 // proofs are compiled in (only at a call's last level, so always with GEN);
 // the plain instantiation carries none of it (the uniform branches cost 2.5 %
 // at C2).
-template <class F, bool GEN, bool FC>
+// SPLIT: a small level's parents split into block-range items (AesArgs::split;
+// never with FC); a separate instantiation so the other levels' kernels carry
+// none of its bookkeeping (in the plain kernel it quadrupled the SGPR spills).
+template <class F, bool GEN, bool FC, bool SPLIT = false>
 __global__ __launch_bounds__(64 * EVAL_WAVES) EVAL_VGPR_ATTR
 void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     typedef typename F::E E;
@@ -739,7 +752,9 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             kc[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_conv + (size_t)i * S, lb));
         }
     }
-    if (threadIdx.x < EVAL_SYNC_WORDS) next_parent[threadIdx.x] = 0u;
+    // words [8, 40): the fused-proof bitmap (FC) or, with split parents, each
+    // parent's first element whose block a lane flagged (split_first below)
+    if (threadIdx.x < EVAL_SYNC_WORDS) next_parent[threadIdx.x] = (SPLIT && threadIdx.x >= 8) ? ~0u : 0u;
     __syncthreads();
     const int aes_waves = a.aes_waves;
     // Proof waves: node proofs of level - 1 (children seeds from cs_in), then
@@ -773,7 +788,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     // every wave through an LDS counter: the proof waves join once their
     // proofs are done, so no wave idles while another still has parents.
     const int wp0 = blockIdx.y * a.par_waves * a.ppw;
-    const int wp1 = min(wp0 + a.par_waves * a.ppw, a.n_parents);
+    const int wp1 = min(wp0 + a.par_waves * a.ppw, SPLIT ? a.n_parents * a.split : a.n_parents);  // items
     // Frontier-cache hit (FC, fuse_proofs == 1): THIS level's node proofs
     // (vidpf.py:366-380, :321-323) of the workgroup's children, overlapped with
     // its parents' AES.  The AES waves [0, aes_waves) walk the parents; a wave
@@ -820,15 +835,6 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     {
     if (a.aes_prio == 1) __builtin_amdgcn_s_setprio(1);
     if (a.aes_prio == 2) __builtin_amdgcn_s_setprio(2);
-    const int run = max(1, a.ppw / 8);
-    auto claim = [&]() -> int {
-        uint32_t o = 0;
-        if (lane == 0) o = atomicAdd(next_parent, (uint32_t)run);
-        return wp0 + (int)__builtin_amdgcn_readfirstlane(o);
-    };
-    int rbeg = claim();
-    if (rbeg >= wp1) goto aes_done;
-    int rend = min(rbeg + run, wp1);
     const int l = a.level;
     const int vl = p.value_len;
     const int wl = vl * F::W32;
@@ -842,10 +848,43 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     const uint32_t ccw = pld(pl.cw_ctrl + (size_t)l * S, lb);
     const uint32_t* wcw = pl.cw_w + (size_t)l * wl * S;
 
+    // Split parents (AesArgs::split, small levels; never FC): pass 0 runs the
+    // items.  A block range that meets a candidate >= p (or the test hook's
+    // block) does not run the exact stream itself -- a rejection shifts every
+    // later element, including other items' ranges, which may already be
+    // stored -- but records its first element in split_first; after a
+    // workgroup barrier, pass 1 re-evaluates each flagged parent with the
+    // exact next_vec stream from that element to the end, overwriting.
+    // (Both children of a parent and all its items are in this workgroup: the
+    // host gives a split level one workgroup per report group.)
+    const int K = SPLIT ? a.split : 1;
+    constexpr int npass = SPLIT ? 2 : 1;
+    const int pb = wp0 / K, pe = (wp1 + K - 1) / K;  // parents of this workgroup
+    uint32_t* const split_first = parent_done;
+    for (int pass = 0; pass < npass; pass++) {
+    if (pass == 1) __syncthreads();  // every item of pass 0 is stored (workgroup fence + barrier)
+    const int run = pass ? 1 : max(1, a.ppw / 8);
+    const int pend = pass ? pe : wp1;
+    auto claim = [&]() -> int {
+        uint32_t o = 0;
+        if (pass == 0) {
+            if (lane == 0) o = atomicAdd(next_parent, (uint32_t)run);
+            return wp0 + (int)__builtin_amdgcn_readfirstlane(o);
+        }
+        for (;;) {  // pass 1: the next flagged parent
+            if (lane == 0) o = atomicAdd(next_parent + 1, 1u);
+            const int q = pb + (int)__builtin_amdgcn_readfirstlane(o);
+            if (q >= pe || __builtin_amdgcn_readfirstlane(split_first[q - pb]) < (uint32_t)p.value_len) return q;
+        }
+    };
+    int rbeg = claim();
+    if (rbeg >= pend) continue;
+    int rend = min(rbeg + run, pend);
     // Parent seed / control bit, software-pipelined one parent ahead so the
     // HBM latency of the child-seed planes hides under the previous parent's
     // AES work.
-    auto load_parent = [&](int pi, uint32_t* ps, uint32_t& pctrl) {
+    auto load_parent = [&](int item, uint32_t* ps, uint32_t& pctrl) {
+        const int pi = (K > 1 && !pass) ? item / K : item;
         if (l == 0) {
 #pragma unroll
             for (int i = 0; i < 4; i++) ps[i] = pld(pl.key + (size_t)i * S, lb);
@@ -860,8 +899,12 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     uint32_t nps[4], npctrl;
     load_parent(rbeg, nps, npctrl);
     for (int item = rbeg; item >= 0;) {
-        const int pi = item;  // parent
-        const int e_lo = 0, e_hi = vl;
+        const int pi = (K > 1 && !pass) ? item / K : item;  // parent
+        const int kp = pass ? 1 : (K > 1 ? item - pi * K : 0);  // its block range (pass 1: no next seeds)
+        constexpr int EPB_ = F::W32 == 2 ? 2 : 1;  // elements per block
+        const int e_lo = pass ? (int)__builtin_amdgcn_readfirstlane(split_first[pi - pb]) : kp * a.split_blocks * EPB_;
+        const int e_hi = (K > 1 && !pass) ? min(vl, e_lo + a.split_blocks * EPB_) : vl;
+        bool deferred = false;  // pass 0 of a split parent met a suspicious block: pass 1 redoes it
         // The key schedules are re-read from LDS (one ds_read_b128 per round):
         // without the barrier the compiler hoists all 22 reads out of the loop
         // and pins 88 VGPRs.
@@ -872,8 +915,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         int nxt = item + 1;
         if (nxt == rend) {
             rbeg = claim();
-            rend = min(rbeg + run, wp1);
-            nxt = rbeg < wp1 ? rbeg : -1;
+            rend = min(rbeg + run, pend);
+            nxt = rbeg < pend ? rbeg : -1;
         }
         if (nxt >= 0) load_parent(nxt, nps, npctrl);
         if constexpr (FC) {
@@ -933,13 +976,13 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         };
         const AesCtrGroup* const gg[2] = {&g0, &g1};
         init_groups(0u);
-        {
+        if (kp == 0) {
             const uint32_t cv[2] = {0u, 0u};
             uint32_t* const ov[2] = {ns0, ns1};
             ctr_blocks_n<2>(TL, rkc, gg, csd, cv, ov);
         }
 #else
-        fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
+        if (kp == 0) fixed_key_block2(TL, rkc, cs0, 0u, cs1, 0u, ns0, ns1);
 #endif
         if constexpr (FC) {
             if (a.cache_out) {
@@ -955,7 +998,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 pst(a.cache_out + (n1 + 4) * CS, lb, tc1);
             }
         }
-        {
+        if (kp == 0) {
             const size_t n0 = (size_t)(2 * pi) * 5, n1 = n0 + 5;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -1053,7 +1096,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
             // stream below redoes this parent from that element on (elements
             // before it are unaffected by the rejection).
             constexpr int EPB = F::W32 == 2 ? 2 : 1;  // elements per block
-            const int nblk = (e_hi + EPB - 1) / EPB;
+            const int nblk = pass ? 0 : (e_hi + EPB - 1) / EPB;  // pass 1: the exact stream only
             for (int b = e_lo / EPB; b < nblk; b++) {
                 asm volatile("" ::: "memory");
                 const int e = EPB * b;
@@ -1082,7 +1125,13 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                     sus = (o0[1] == ~0u) | (o1[1] == ~0u) | (two & ((o0[3] == ~0u) | (o1[3] == ~0u)));
                 else
                     sus = (o0[3] == ~0u) | (o1[3] == ~0u);
-                if (__builtin_expect(__any(sus), 0) || b == a.force_slow_blk) break;
+                if (__builtin_expect(__any(sus), 0) || b == a.force_slow_blk) {
+                    if (K > 1) {
+                        if (lane == 0) atomicMin(split_first + (pi - pb), (uint32_t)e);
+                        deferred = true;
+                    }
+                    break;
+                }
                 // All of this block's loads (issued before its AES) and the
                 // previous block's stores have long completed: say so with one
                 // explicit wait.  Otherwise the waitcnt pass, which loses track
@@ -1099,7 +1148,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 e_fast = e + 1 + (two ? 1 : 0);
             }
         }
-        if (e_fast < e_hi) {
+        if (e_fast < e_hi && !deferred) {
             // exact next_vec streams (rejection sampling), element by element
             // from the stream's start (a rejection shifts every later element)
             // up to e_hi, emitting from e_fast on; elements before it were
@@ -1123,6 +1172,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
         }
         item = nxt;
     }
+    }  // pass
     }
 aes_done:
     if constexpr (FC) {

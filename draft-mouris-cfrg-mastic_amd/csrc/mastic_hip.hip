@@ -185,7 +185,18 @@ struct mastic_ctx {
     DevBuf agg_valid, agg_out;  // mastic_aggregate staging
     DevBuf agg_part;            // per-chunk partial sums of a split fold (aggregate_impl)
     DevBuf stage;               // result encoding / decide staging
-    bool absorb_pair = true;    // two lanes per binder sponge (MASTIC_ABSORB_SINGLE=1: one)
+    // Lanes per binder sponge.  Two (k_absorb_pair: half the dependent chain
+    // per permutation, ~1.5x the VALU issue slots) while the chains are the
+    // critical path, i.e. a chunk of few reports (C2's 16,384: one sponge wave
+    // for every second SIMD); one (k_absorb: a third fewer VALU slots taken
+    // from the level kernel beside it) once a chunk has enough reports for the
+    // sponges to be throughput-bound (the 1M-report sweep's ~380k-report
+    // chunks).  Same-box A/B (profiles/r05_v6_ab_single_lane_sponges.txt): one
+    // lane is +4.5 % on the 1M sweep, -2 % on C2 and -21 % on C5 at 16,384.
+    // 0 = by chunk size (>= absorb_single_min reports: one lane), 1 = always
+    // one, 2 = always two (MASTIC_ABSORB_SINGLE).
+    int absorb_mode = 0;
+    size_t absorb_single_min = 65536;  // MASTIC_ABSORB_SINGLE_MIN
     int absorb_lds = 0;         // bytes of dynamic LDS per absorb workgroup (MASTIC_ABSORB_LDS_KB)
     int n_cus = 256;                     // compute units of the device
     int proof_waves = EVAL_PROOF_WAVES;  // proof waves per eval workgroup (MASTIC_PROOF_WAVES)
@@ -222,6 +233,7 @@ struct mastic_ctx {
     bool fuse_last_miss_fc = true;  // ... a cache-on miss's (MASTIC_FUSE_LAST_MISS_FC=0: k_node_proof)
     bool hit_absorb_main = true;  // a single-chunk hit's sponges on the main stream (MASTIC_HIT_ABSORB_MAIN=0: sponge stream)
     bool fc_all = false;        // A/B only: the frontier-cache kernel variant at every level (MASTIC_FC_ALL=1)
+    bool small_split = true;    // small levels' parents split into block-range items (MASTIC_SMALL_SPLIT=0: off)
     int fuse_proofs = 1;        // last level's node proofs in the level kernel, overlapped with its AES: 1 on
                                 // cache hits, 2 also on cache-on misses, 0 never (MASTIC_FUSE_PROOFS; else
                                 // k_node_proof); 3 (A/B): on hits, after a workgroup barrier
@@ -663,6 +675,30 @@ static int choose_eval_ppw(int n_parents, int groups, int aes_waves, int n_cus) 
     return best;
 }
 
+// Items per parent at a small level (AesArgs::split).  A workgroup's 16
+// waves share its items; a parent's AES is 2 extend blocks plus nblk convert
+// blocks per child (next seed + payload: 2 + 2 nblk in lockstep pairs).  With
+// few parents the launch time is the workgroup's longest serial chain:
+// items per wave x blocks per item.  Pick the split minimising that (each
+// item recomputes the extend pair; item 0 adds the next-seed pair), fewer
+// items on ties.  At 16 or more parents this is 1 (no split).
+static void choose_split(int n_parents, int nblk, int* split, int* split_blocks) {
+    int best_k = 1, best_cost = 1 << 30;
+    for (int k = 1; k <= nblk; k++) {
+        const int nb = (nblk + k - 1) / k;
+        const int kk = (nblk + nb - 1) / nb;  // ranges actually non-empty
+        if (kk != k) continue;
+        const int per_wave = (n_parents * k + EVAL_WAVES - 1) / EVAL_WAVES;
+        const int cost = per_wave * (2 + 2 * nb) + 2;
+        if (cost < best_cost) {
+            best_cost = cost;
+            best_k = k;
+        }
+    }
+    *split = best_k;
+    *split_blocks = (nblk + best_k - 1) / best_k;
+}
+
 static int copy_planes(mastic_ctx* c, DevBuf& dst, size_t dst_stride, size_t dst_off, const uint32_t* src,
                        size_t src_stride, size_t n, size_t planes, hipStream_t s) {
     if (planes == 0) return 0;
@@ -790,6 +826,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     auto pay_gs = [&](int) -> int { return pay_gstride; };
     // Sponges which0 .. which0 + nwh - 1 (0 one-hot, 1 payload) of level lv on
     // stream `as` after `ready`; *done marks their end.
+    const bool pair = c->absorb_mode == 2 || (c->absorb_mode == 0 && (size_t)n < c->absorb_single_min);
     auto launch_sponges = [&](int lv, int which0, int nwh, hipEvent_t ready, hipEvent_t e4, hipEvent_t e5,
                               hipStream_t as, hipEvent_t* done) -> int {
         AbsorbArgs ab;
@@ -809,7 +846,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         if (e4) HIPCHK(c, hipEventRecord(e4, as));
         if (c->dbg_skip & 4) {
             // timing experiments only: no binder sponges (results wrong)
-        } else if (c->absorb_pair)
+        } else if (pair)
             hipLaunchKernelGGL(k_absorb_pair,
                                dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, (unsigned)nwh),
                                dim3(c->absorb_threads), c->absorb_lds, as, pl, ab);
@@ -898,8 +935,23 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         // all waves parents from the start: measured neutral on C4 and C2 and
         // 3 % slower on C5 (profiles/r02_v12_ab_level_kernel.json)
         const int par_waves = c->par_waves > 0 ? c->par_waves : EVAL_WAVES - c->proof_waves;
-        const int n_items = np_;
+        // small levels: parents split into block-range items (AesArgs::split);
+        // not at the last level (out shares, frontier-cache staging) nor on a hit
+        a.split = 1;
+        a.split_blocks = 0;
+        {
+            const int epb = p.field == 64 ? 2 : 1;
+            const int nblk = (p.value_len + epb - 1) / epb;
+            a.split_blocks = nblk;
+            // (<= 32 parents: their pass-0 flags live in the workgroup's sync words)
+            if (!hit && l < t->L && c->small_split && np_ <= 32 && !(c->dbg_skip & 2))
+                choose_split(np_, nblk, &a.split, &a.split_blocks);
+        }
+        const int n_items = np_ * a.split;
         a.ppw = choose_eval_ppw(n_items, groups, par_waves, c->n_cus);
+        // a split level keeps all items of a report group in one workgroup
+        // (the fix-up pass needs every item of a parent stored): gy = 1
+        if (a.split > 1) a.ppw = (n_items + par_waves - 1) / par_waves;
         a.parent_node = t->d_parent + t->poff[l];
         a.child_exp = t->d_exp + t->off[l];
         a.child_pfx = t->d_pfx + t->off[l];
@@ -958,6 +1010,12 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         if ((lc && (hit || l == t->L || c->fc_all)) || fuse)
             hipLaunchKernelGGL((k_eval_aes<F, true, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
                                p, pl, a);
+        else if (a.split > 1 && l == 0)
+            hipLaunchKernelGGL((k_eval_aes<F, true, false, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES,
+                               c->stream, p, pl, a);
+        else if (a.split > 1)
+            hipLaunchKernelGGL((k_eval_aes<F, false, false, true>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES,
+                               c->stream, p, pl, a);
         else if (l == 0 || l == t->L)
             hipLaunchKernelGGL((k_eval_aes<F, true, false>), grid, dim3(64 * EVAL_WAVES), EVAL_LDS_BYTES, c->stream,
                                p, pl, a);
@@ -2082,7 +2140,9 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     // MASTIC_DBG_SKIP and MASTIC_ABSORB_DBG skip or gut kernels: results wrong.
     {
         const char* e = getenv("MASTIC_ABSORB_SINGLE");
-        c->absorb_pair = !(e && e[0] == '1');
+        if (e) c->absorb_mode = e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
+        const char* esm = getenv("MASTIC_ABSORB_SINGLE_MIN");
+        if (esm) c->absorb_single_min = (size_t)std::max(0, atoi(esm));
         const char* l = getenv("MASTIC_ABSORB_LDS_KB");
         c->absorb_lds = l ? std::max(0, std::min(160, atoi(l))) * 1024 : 0;
         const char* pw = getenv("MASTIC_PROOF_WAVES");
@@ -2125,6 +2185,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (flf) c->fuse_last_miss_fc = flf[0] != '0';
         const char* ham = getenv("MASTIC_HIT_ABSORB_MAIN");
         if (ham) c->hit_absorb_main = ham[0] != '0';
+        const char* ssp = getenv("MASTIC_SMALL_SPLIT");
+        if (ssp) c->small_split = ssp[0] != '0';
     }
 #endif
     // the level kernel's LDS (table + key schedules) is dynamic, above the
@@ -2141,6 +2203,14 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
                             EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_eval_aes<F128, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F64, true, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F64, false, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, true, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, EVAL_LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_eval_aes<F128, false, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_absorb_pair, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess) {
         delete c;
