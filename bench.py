@@ -650,6 +650,11 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
                     "(which run beside the level kernels)",
         },
         "breakdown_ms_per_step": {
+            # every algorithmic op of the AES and Keccak kernels (level kernels: nodes x ops per
+            # node; binder sponges: their Keccak-p) over the sweep's wall time (host gaps included)
+            # (this rank's work over the job's wall time: per-GPU utilisation)
+            "frac_int_valu_whole_sweep": (nodes * dom_ops + ab_perms * steps * KECCAK_OPS) / dt / 1e12
+            / VALU_PEAK_TOPS,
             "eval_aes_plus_proofs": dom_ms / steps,
             "absorb": sum(t[4] for t in timing) / steps,
             "prep_init_total": sum(t[6] for t in timing) / steps,
@@ -1217,6 +1222,7 @@ def main():
             "heavy_hitters_equal_plaintext": nc["heavy_hitters_equal_plaintext"],
             "frac": ns["roofline"]["frac"],
             "frac_executed": ns["roofline"]["frac_executed"],
+            "frac_int_valu_whole_sweep": ns["breakdown_ms_per_step"]["frac_int_valu_whole_sweep"],
             "roofline_absorb": ns["roofline_absorb"],
             "roofline_kernel": ns["roofline"]["kernel"],
             "per_level": ns["per_level"],
