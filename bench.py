@@ -886,7 +886,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
+    # under torch.distributed.run (the driver's N > 1 launch; also at one rank) the ranks form a
+    # process group, even of one
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         # The control plane (barriers, the max over ranks, the communicator id)
         # runs over gloo; the data path's all-gather of agg shares runs on the
@@ -954,7 +956,7 @@ def main():
 
     def step(reps):
         m.prep_init_device(reps, vk, ctx, args.agg_id, enc_ap)
-        if world > 1 and lib_comm:
+        if dist is not None and lib_comm:
             # agg share folded into HBM, all-gathered over the library's RCCL
             # communicator and merged mod p on the GPU, in one call
             return m.aggregate_merged((args.agg_id,), n_elems)
@@ -1118,7 +1120,7 @@ def main():
                 print("[full_job] %d / %d slices, %.0f s" % (j + 1, len(bounds), t_last - t1), file=sys.stderr,
                       flush=True)
         job = fold_on_gpu(m, torch.cat(parts), len(parts), n_elems)
-        if world > 1 and lib_comm:
+        if dist is not None and lib_comm:
             merged = torch.empty_like(job)
             m.allgather_fold(job.data_ptr(), 1, n_elems, merged.data_ptr(), torch.cuda.current_stream().cuda_stream)
             job = merged

@@ -75,3 +75,30 @@ def test_bench_four_ranks_one_rank_without_reports():
     c = d["config"]
     assert d["n_gpus"] == 4 and c["job_reports"] == 3 and c["reports_this_rank"] == 0
     assert c["heavy_hitters_equal_plaintext"] is True
+
+
+def test_bench_under_torchrun_uses_the_library_communicator():
+    """The driver's N > 1 launch path at one rank: torch.distributed.run starts
+    bench.py, the ranks form a gloo control group, and every agg-share merge
+    (C2 steps, the full job, the north_star sweep's per-level totals) goes
+    through the library's own RCCL communicator (mastic_comm_init with one
+    rank, mastic_aggregate_merged / mastic_allgather_fold, CommMerge)."""
+    import socket
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "1",
+           "--warmup", "1", "--reports", "1024", "--total-reports", "2048", "--north-star-reports", "16384",
+           "--cpu-baseline", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert "mastic_allgather_fold" in d["full_job"]["what"]
+    ns = d["north_star"]
+    assert ns["job_reports"] == 16384 and ns["heavy_hitters_equal_plaintext"] is True
