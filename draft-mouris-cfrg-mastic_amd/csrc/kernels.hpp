@@ -1328,7 +1328,12 @@ __global__ __launch_bounds__(256) void k_absorb(Planes pl, AbsorbArgs a) {
         if (!full) break;
         asm volatile("" ::: "memory");
         if (more) load_block(b + 1, cur);
-        keccak_p12(s);
+#ifdef MASTIC_EXPERIMENT_KNOBS
+        if (a.dbg == 3)
+            keccak_p12<2>(s);  // A/B only: rolled rounds (small code; same results)
+        else
+#endif
+            keccak_p12(s);
         if (!more) break;
     }
 #pragma unroll

@@ -50,6 +50,22 @@
 #define LSHL(r) asm volatile("v_lshlrev_b32 %0, 7, %0" : "+v"(r));
 #define XORDPP(r) asm volatile("v_xor_b32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
 #define CND(r) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r) : "v"(k));
+#define MOVDPP(r) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r));
+// lane i <-> i+32 / i+16 half exchanges (gfx950): one instruction writes both registers of a pair;
+// counted below as one wave-instruction per swap (4 swaps per 8 registers per iteration, so the
+// kernel runs twice the iterations to issue as many instructions as the others)
+#define PL32(x, y) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+#define PL16(x, y) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+#define PAIRS(OP) OP(a0, a1) OP(a2, a3) OP(a4, a5) OP(a6, a7)
+#define KERNELPAIR(NAME, OP)                                                             \
+    __global__ __launch_bounds__(256) void NAME(uint32_t* out, uint32_t seed) {          \
+        uint32_t k = seed ^ threadIdx.x;                                                  \
+        uint32_t a0 = k, a1 = k + 1, a2 = k + 2, a3 = k + 3, a4 = k + 4, a5 = k + 5,     \
+                 a6 = k + 6, a7 = k + 7;                                                  \
+        for (int i = 0; i < 2 * ITERS; i++) { PAIRS(OP) }                                \
+        uint32_t s = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;                               \
+        if (s == 0x12345678u) out[blockIdx.x * 256 + threadIdx.x] = s;                    \
+    }
 
 #define KERNEL(NAME, OP)                                                                 \
     __global__ __launch_bounds__(256) void NAME(uint32_t* out, uint32_t seed) {          \
@@ -99,6 +115,9 @@ KERNEL(k_add3, ADD3)
 KERNEL(k_lshl, LSHL)
 KERNEL(k_xordpp, XORDPP)
 KERNEL(k_cnd, CND)
+KERNEL(k_movdpp, MOVDPP)
+KERNELPAIR(k_pl32, PL32)
+KERNELPAIR(k_pl16, PL16)
 
 int main() {
     hipDeviceProp_t prop;
@@ -120,7 +139,8 @@ int main() {
               {"v_pk_mad_u16", k_pkmad16}, {"v_pk_lshlrev_b16", k_pklshl16}, {"v_mad_u32_u24", k_mad24},
               {"v_mul_u32_u24", k_mul24}, {"v_or3_b32", k_xor3}, {"v_lshl_add_u32", k_lshladd},
               {"v_add3_u32", k_add3}, {"v_lshlrev_b32", k_lshl}, {"v_xor_b32_dpp", k_xordpp},
-              {"v_cndmask_b32", k_cnd}};
+              {"v_cndmask_b32", k_cnd}, {"v_mov_b32_dpp(quad_perm swap)", k_movdpp},
+              {"v_permlane32_swap_b32", k_pl32}, {"v_permlane16_swap_b32", k_pl16}};
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
