@@ -770,7 +770,19 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     if (hit)
         HIPCHK(c, hipMemsetAsync(pl.status, 0, (size_t)stride * 4, c->stream));
     else {
-        HIPCHK(c, hipMemsetAsync(W, 0, wl.cs[0] * (size_t)stride * 4, c->stream));
+        // Of the header, the keys, nonces and correction words (k_unpack: every
+        // report row, every level the call reads) and the AES key schedules and
+        // sponge states (k_setup: every row) are written in full before any
+        // read, so only their padding rows are cleared; the planes between
+        // (leader proof share, seeds: by aggregator and circuit) and from the
+        // root sum on (accumulated root sum and FLP, result and status planes)
+        // are cleared whole.  C2: 409 of 2,107 header words per report.
+        // (work_layout order: key, nonce, cw_* | lps, seed, peer | rk_*, sp_* | rootsum .. status)
+        HIPCHK(c, hipMemsetAsync(W + wl.lps * (size_t)stride, 0, (wl.rk_ext - wl.lps) * (size_t)stride * 4, c->stream));
+        HIPCHK(c, hipMemsetAsync(W + wl.rootsum * (size_t)stride, 0, (wl.cs[0] - wl.rootsum) * (size_t)stride * 4,
+                                 c->stream));
+        if (stride > n)
+            HIPCHK(c, hipMemset2DAsync(W + n, (size_t)stride * 4, 0, (size_t)(stride - n) * 4, wl.lps, c->stream));
         // level 0 reads its parent (the root) payload from fr_w[1]: zeros
         HIPCHK(c, hipMemsetAsync(W + wl.fr_w[1] * (size_t)stride, 0, (size_t)p.value_len * p.w32 * stride * 4, c->stream));
     }
