@@ -1823,6 +1823,12 @@ extern "C" int mastic_last_timing3(mastic_ctx* c, double* aes_ms, int* aes_launc
     if (!c) return MASTIC_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->tm[c->tcur].n_eval < 0) {
+        // some timing marks sit on the sponge streams without the main stream
+        // waiting for them (a single-chunk hit's empty sponge marks, recorded
+        // on the sponge stream while its sponges run on the main stream):
+        // wait for the marks themselves (an unwaited mark gave "device not
+        // ready" in a 4-rank run sharing one GPU)
+        for (int i = 0; i < -c->tm[c->tcur].n_eval; i++) HIPCHK(c, hipEventSynchronize(c->tm[c->tcur].ev[i]));
         // events: [t0, t1] then per level [aes0, aes1, proof0, proof1, absorb0, absorb1]
         const size_t evi = (size_t)(-c->tm[c->tcur].n_eval);
         double ta = 0, tp = 0, tb = 0;

@@ -29,6 +29,7 @@ def test_bench_two_ranks_on_one_gpu():
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["full_job"]["job_reports"] == 4096
     ns = d["north_star"]
+    assert "error" not in ns, ns
     assert ns["n_gpus"] == 2 and ns["scaling"] == "strong" and ns["job_reports"] == 16384
     assert ns["heavy_hitters_equal_plaintext"] is True
 
@@ -40,7 +41,12 @@ def _run_bench(args, timeout=500):
     # the failing rank's own traceback, not only the launcher's tail
     first = "\n".join(l for l in r.stderr.splitlines() if l.startswith("[rank0]") or "Error" in l)[:4000]
     assert r.returncode == 0, first + "\n...\n" + r.stderr[-1500:]
-    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    # a rank whose north_star leg raised prints its traceback and leaves the
+    # others' collectives ("Connection closed by peer"): show every rank's
+    tb = [l for l in r.stderr.splitlines() if "Error" in l or "Traceback" in l or l.lstrip().startswith("File ")]
+    assert "error" not in d.get("north_star", {}), (d["north_star"], "\n".join(tb)[-6000:])
+    return d
 
 
 def test_bench_four_ranks_uneven_job_on_one_gpu():
@@ -101,4 +107,5 @@ def test_bench_under_torchrun_uses_the_library_communicator():
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert "mastic_allgather_fold" in d["full_job"]["what"]
     ns = d["north_star"]
+    assert "error" not in ns, ns
     assert ns["job_reports"] == 16384 and ns["heavy_hitters_equal_plaintext"] is True
