@@ -126,9 +126,11 @@ MH_D void unpack_words(const uint8_t* src, int nw, uint32_t* dst, size_t step) {
 // Wire public share: pack_bits(ctrl) || seed_cw[B] || w_cw[B] || proof_cw[B]
 // (poc/vidpf.py:382-394).  Input share: key || [leader proof share] || [seed]
 // || [peer jr part] (poc/mastic.py:516-529).
+// big = false: every segment; big = true: the correction words and the
+// leader proof share are left to k_rows_to_planes (coalesced row tiles).
 template <int A>
 MH_D void unpack_report(const McParams& p, const Planes& pl, int agg_id, int r, const uint8_t* ps, const uint8_t* is,
-                        const uint8_t* nc, int l_lo, int l_hi) {
+                        const uint8_t* nc, int l_lo, int l_hi, bool big = false) {
     const size_t S = (size_t)pl.stride;
     const int nctrl = (2 * p.bits + 7) / 8;
     const int wl = p.value_len * p.w32;
@@ -138,6 +140,7 @@ MH_D void unpack_report(const McParams& p, const Planes& pl, int agg_id, int r, 
         uint32_t c0 = (ps[(2 * l) >> 3] >> ((2 * l) & 7)) & 1;
         uint32_t c1 = (ps[(2 * l + 1) >> 3] >> ((2 * l + 1) & 7)) & 1;
         pl.cw_ctrl[(size_t)l * S + r] = c0 | (c1 << 1);
+        if (big) continue;
         unpack_words<A>(ps + nctrl + 16 * l, 4, pl.cw_seed + (size_t)l * 4 * S + r, S);
         unpack_words<A>(ps + nctrl + 16 * p.bits + (size_t)l * p.value_len * p.enc, wl,
                         pl.cw_w + (size_t)l * wl * S + r, S);
@@ -146,7 +149,7 @@ MH_D void unpack_report(const McParams& p, const Planes& pl, int agg_id, int r, 
     }
     const uint8_t* q = is + 16;
     if (agg_id == 0) {
-        unpack_words<A>(q, p.proof_len * p.w32, pl.lps + r, S);
+        if (!big) unpack_words<A>(q, p.proof_len * p.w32, pl.lps + r, S);
         q += (size_t)p.proof_len * p.enc;
     }
     if (agg_id == 1 || p.joint_rand_len > 0) {
@@ -157,7 +160,8 @@ MH_D void unpack_report(const McParams& p, const Planes& pl, int agg_id, int r, 
 }
 
 __global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_id, const uint8_t* nonces,
-                                                const uint8_t* pub, const uint8_t* ins, int l_lo, int l_hi) {
+                                                const uint8_t* pub, const uint8_t* ins, int l_lo, int l_hi,
+                                                int big) {
     // correction words of levels l_lo .. l_hi-1 only: a call at level L never
     // reads deeper ones, and a frontier-cache hit only reads level L's
     const int r = blockIdx.x * 256 + threadIdx.x;
@@ -171,9 +175,46 @@ __global__ __launch_bounds__(256) void k_unpack(McParams p, Planes pl, int agg_i
     // every segment offset is nctrl plus multiples of 8 bytes (enc is 8 or 16)
     const bool a8 = (((uintptr_t)pub | (uintptr_t)ins | (uintptr_t)nonces | ps_size | is_size | nctrl) & 7) == 0;
     if (a8)
-        unpack_report<8>(p, pl, agg_id, r, ps, is, nc, l_lo, l_hi);
+        unpack_report<8>(p, pl, agg_id, r, ps, is, nc, l_lo, l_hi, big != 0);
     else
         unpack_report<1>(p, pl, agg_id, r, ps, is, nc, l_lo, l_hi);
+}
+
+// Words [0, nwords) of every report's wire row (row r at src + r * row_bytes,
+// 8-byte aligned) into plane rows: dst[j * S + r] = word j of row r.  With one
+// lane per report (k_unpack) every load of a wave touches 64 rows, i.e. 64
+// cache lines for 8 bytes each (C5: 32 ms for its 526 KB public shares at
+// 16,384 reports, ~0.5 TB/s); here a workgroup moves a tile of 64 reports x
+// 64 words through LDS: each half-wave reads 256 contiguous bytes of one row,
+// each wave writes 256 contiguous bytes of one plane row.
+__global__ __launch_bounds__(256) void k_rows_to_planes(const uint8_t* src, size_t row_bytes, int n, int nwords,
+                                                        uint32_t* dst, int S) {
+    __shared__ uint32_t tile[64 * 65];  // [report][word], pitch 65: the transposed reads hit 64 banks
+    const int r0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int q = k * 256 + t;
+        const int rr = q >> 5, wp = q & 31;  // report of the tile, word pair
+        const int j = j0 + 2 * wp;
+        uint2 v = make_uint2(0u, 0u);
+        if (r0 + rr < n) {
+            const uint8_t* row = src + (size_t)(r0 + rr) * row_bytes;
+            if (j + 1 < nwords)
+                v = *(const uint2*)(row + 4 * (size_t)j);
+            else if (j < nwords)
+                v.x = *(const uint32_t*)(row + 4 * (size_t)j);
+        }
+        tile[rr * 65 + 2 * wp] = v.x;
+        tile[rr * 65 + 2 * wp + 1] = v.y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int q = k * 256 + t;
+        const int jj = q >> 6, rr = q & 63;
+        if (r0 + rr < n && j0 + jj < nwords) dst[(size_t)(j0 + jj) * S + r0 + rr] = tile[rr * 65 + jj];
+    }
 }
 
 // ------------------------------------------------------------- key setup

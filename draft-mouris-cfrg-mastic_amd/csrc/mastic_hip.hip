@@ -789,9 +789,41 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
     const size_t ps = mc_public_share_size(p), is = mc_input_share_size(p, agg_id);
     const uint8_t* ins = agg_id == 0 ? rep->in0.as<uint8_t>() : rep->in1.as<uint8_t>();
     const PrefixState* pfx = (const PrefixState*)c->pfx.p;
-    hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
-                       rep->nonces.as<uint8_t>() + 16 * base, rep->pub.as<uint8_t>() + ps * base, ins + is * base,
-                       hit ? t->L - 1 : 0, t->L + 1);  // a hit recomputes level L-1's payloads: its CW
+    {
+        const uint8_t* pub = rep->pub.as<uint8_t>() + ps * base;
+        const uint8_t* in_b = ins + is * base;
+        const int l_lo = hit ? t->L - 1 : 0, l_hi = t->L + 1;  // a hit recomputes level L-1's payloads: its CW
+        // Rows of >= 16 KB to unpack per report (C4, C5), 8-byte aligned
+        // (BITS a multiple of 32): the correction words and the leader proof
+        // share, the bulk of a report's bytes, go through coalesced row tiles;
+        // k_unpack keeps the nonce, key, control bits and seeds.  Same-box A/B
+        // (profiles/r05_v37_ab_row_tile_unpack.txt): C5 +2.2 %, C4 +0.5 %;
+        // the 1M sweep's rows (<= 5.9 KB) gained nothing in wall time (+0.1 %)
+        // while its level kernels, started earlier under the previous chunk's
+        // sponges, measured 1.3 % longer, so small rows keep one lane per report.
+        const size_t nctrl = (2 * (size_t)p.bits + 7) / 8;
+        const size_t row_bytes = (size_t)(l_hi - l_lo) * (16 + (size_t)p.value_len * p.enc + 32) +
+                                 (agg_id == 0 ? (size_t)p.proof_len * p.enc : 0);
+        const bool tiles = row_bytes >= 16384 && (((uintptr_t)pub | (uintptr_t)in_b | ps | is | nctrl) & 7) == 0 &&
+                           (size_t)p.value_len * p.w32 * (l_hi - l_lo) / 64 < 65535;  // grid y
+        hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
+                           rep->nonces.as<uint8_t>() + 16 * base, pub, in_b, l_lo, l_hi, tiles ? 1 : 0);
+        if (tiles) {
+            const int wlw_ = p.value_len * p.w32, nl = l_hi - l_lo;
+            auto rows = [&](const uint8_t* src, size_t row_bytes, int nwords, uint32_t* dst) {
+                if (nwords <= 0) return;
+                hipLaunchKernelGGL(k_rows_to_planes, dim3((unsigned)((n + 63) / 64), (unsigned)((nwords + 63) / 64)),
+                                   dim3(256), 0, c->stream, src, row_bytes, n, nwords, dst, stride);
+            };
+            const uint8_t* seg = pub + nctrl;
+            rows(seg + 16 * (size_t)l_lo, ps, 4 * nl, pl.cw_seed + (size_t)4 * l_lo * stride);
+            seg += 16 * (size_t)p.bits;
+            rows(seg + (size_t)l_lo * p.value_len * p.enc, ps, wlw_ * nl, pl.cw_w + (size_t)wlw_ * l_lo * stride);
+            seg += (size_t)p.bits * p.value_len * p.enc;
+            rows(seg + 32 * (size_t)l_lo, ps, 8 * nl, pl.cw_proof + (size_t)8 * l_lo * stride);
+            if (agg_id == 0) rows(in_b + 16, is, p.proof_len * p.w32, pl.lps);
+        }
+    }
     const bool whole = base == 0 && (size_t)n == rep->n && W == c->work.p;
     const bool rk_ok = hit && whole && c->rk.valid && c->rk.rep_id == rep->id && c->rk.rep_gen == rep->generation() &&
                        c->rk.n == (size_t)n && c->rk.stride == stride && c->rk.W == (const void*)W &&
