@@ -169,6 +169,7 @@ struct mastic_ctx {
     hipStream_t stream = nullptr;   // level evals, setup, finalize, FLP
     hipStream_t stream2 = nullptr;  // binder sponges (overlap the next level's eval)
     hipStream_t stream3 = nullptr;  // binder sponges of the odd chunks of a pipelined prep_init
+    hipStream_t stream4 = nullptr;  // FLP randomness + query of a weight-check call, beside its last sponges
     std::vector<hipEvent_t> sync_ev;
     hipEvent_t fold_ev = nullptr;  // mastic_fold_shares: producer stream -> stream
     // library-owned RCCL communicator (mastic_comm_init; none = world 1)
@@ -226,7 +227,7 @@ struct mastic_ctx {
     // still read, so they must not rely on hipFree's implicit device wait).
     bool idle() {
         return hipStreamSynchronize(stream) == hipSuccess && hipStreamSynchronize(stream2) == hipSuccess &&
-               hipStreamSynchronize(stream3) == hipSuccess;
+               hipStreamSynchronize(stream3) == hipSuccess && hipStreamSynchronize(stream4) == hipSuccess;
     }
     int split_sponges = -1;  // payload sponge a level earlier, on the third stream: -1 Field128 only, 0 never, 1 always (MASTIC_SPLIT_SPONGES)
     bool fuse_last_miss = false;    // any miss's last level with fused, overlapped node proofs (MASTIC_FUSE_LAST_MISS=1)
@@ -295,6 +296,7 @@ struct mastic_ctx {
         if (stream) (void)hipStreamDestroy(stream);
         if (stream2) (void)hipStreamDestroy(stream2);
         if (stream3) (void)hipStreamDestroy(stream3);
+        if (stream4) (void)hipStreamDestroy(stream4);
     }
 };
 
@@ -1130,17 +1132,33 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                   : launch_absorb(l, np_done, e4, e5, last_as))
             return -1;
     }
+    hipEvent_t flp_done = nullptr;
+    if (t->weight_check) {
+        // The FLP randomness and query (mastic.py:234-256) read only header
+        // planes and level 0's root sum: on their own stream once the last
+        // level kernel is done, beside the last level's sponges (a few
+        // latency-bound chains that leave most of the chip idle: C5's last
+        // payload chain runs ~34 ms) instead of after them.  (Right after
+        // level 0 they slowed the level kernels beside them by as much as
+        // they saved: C4 -1.8 %, profiles/r05_v36_ab_flp_side_stream.txt.)
+        hipEvent_t lv_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(lv_done, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream4, lv_done, 0));
+        FlpArgs fl{agg_id, t->L};
+        hipLaunchKernelGGL(k_flp_rand<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream4, p, pl, fl, pfx);
+        hipLaunchKernelGGL(k_flp_query<F>, dim3((stride + 255) / 256), dim3(256), 0, c->stream4, p, pl,
+                           flp_consts<F>(p));
+        HIPCHK(c, hipGetLastError());
+        flp_done = get_sync_event(c, sev++);
+        HIPCHK(c, hipEventRecord(flp_done, c->stream4));
+    }
     if (tail != last_as) HIPCHK(c, hipStreamWaitEvent(tail, abs_done[t->L], 0));
     if (split && pl_done[t->L]) HIPCHK(c, hipStreamWaitEvent(tail, pl_done[t->L], 0));
     FinalArgs fa{agg_id, f_oh, f_pl};
     hipLaunchKernelGGL(k_finalize<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl, fa, pfx);
-    if (t->weight_check) {
-        FlpArgs fl{agg_id, t->L};
-        hipLaunchKernelGGL(k_flp_rand<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl, fl, pfx);
-        hipLaunchKernelGGL(k_flp_query<F>, dim3((stride + 255) / 256), dim3(256), 0, tail, p, pl,
-                           flp_consts<F>(p));
-    }
     HIPCHK(c, hipGetLastError());
+    // the status, verifier and joint-rand planes copied below are the FLP's
+    if (flp_done) HIPCHK(c, hipStreamWaitEvent(tail, flp_done, 0));
     if (lc && !direct) {
         // frontier cache for the next level (the last level's nodes are in the
         // spare slot already, written by its level kernel): the root sum
@@ -1372,7 +1390,7 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     const bool pipe = c->chunk_pipeline && n > chunk && chunk >= 128 && half_cap >= pad + 64;
     if (pipe) chunk = std::min(capped ? chunk : chunk / 2, half_cap - pad) / 64 * 64;
     const size_t half = c->work.bytes / 2 / 4 / 64 * 64;  // words: second half's offset
-    const size_t nsev = 2 * (size_t)t->L + 8;           // sync events one chunk uses
+    const size_t nsev = 3 * (size_t)t->L + 12;          // sync events one chunk uses
     size_t evi = 0;
     hipEvent_t t0 = get_event(c, evi++), t1 = get_event(c, evi++);
     HIPCHK(c, hipEventRecord(t0, c->stream));
@@ -2272,7 +2290,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+        hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MASTIC_EHIP;
     }
@@ -2286,6 +2305,7 @@ extern "C" void mastic_ctx_destroy(mastic_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamSynchronize(c->stream3);
+    (void)hipStreamSynchronize(c->stream4);
     delete c;
 }
 
