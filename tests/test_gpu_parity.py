@@ -288,6 +288,48 @@ def test_chunked_batches_equal_unchunked(mastic_amd, chunk_groups, n):
     assert m.aggregate_device(0, ap) == agg_full
 
 
+def test_chunked_field128_large_rows_equal_unchunked_and_oracle(mastic_amd):
+    """Field128 with rows of >= 16 KB to unpack per report (SumVec(64) to
+    level 15: 16 x 1,088 B of correction words -- the coalesced row-tile
+    unpack, k_rows_to_planes), a weight check (the FLP on its own stream beside
+    the last sponges) and 256-report chunks pipelined as 128-report halves
+    (their tails on the sponge streams): prep shares and out shares of both
+    aggregators equal the unchunked call's, and sampled reports equal the
+    oracle's."""
+    import ctypes
+    from mastic_amd import _lib
+    rng = random.Random(21)
+    m = mastic_amd.MasticSumVec(32, 64, 1, 8)
+    o = _oracle_for(m)
+    n = 600
+    (alphas, weights, nonces, rands) = _random_reports(m, rng, n)
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    ap = _random_agg_param(m, rng, alphas, 15, 24, True)
+    vk = bytes(range(32))
+    enc = m.encode_agg_param(ap)
+    per = ctypes.c_uint64()
+    assert _lib.lib().mastic_work_bytes(m._ctx, enc, len(enc), ctypes.byref(per)) == 0
+    psz, isz = m.public_share_size(), [m.input_share_size(0), m.input_share_size(1)]
+    for a in range(2):
+        ins = in0 if a == 0 else in1
+        full = m.prep_init_batch(vk, CTX, a, ap, nonces, pub, ins)
+        try:
+            _lib.lib().mastic_set_memory_budget(m._ctx, (64 * 4 + 64) * per.value + 1000)
+            chunked = m.prep_init_batch(vk, CTX, a, ap, nonces, pub, ins)
+        finally:
+            _lib.lib().mastic_set_memory_budget(m._ctx, 0)
+        assert chunked[0] == full[0] and chunked[2] == full[2], "agg %d" % a
+        assert list(chunked[3]) == list(full[3])
+        pss = m.prep_share_size(True)
+        osz = len(full[2]) // n
+        for i in (0, 301, n - 1):  # first chunk, second chunk (other arena half), last (partial) chunk
+            cw = o.vidpf.decode_public_share(pub[psz * i:psz * (i + 1)])
+            ish = o.decode_input_share(a, ins[isz[a] * i:isz[a] * (i + 1)])
+            (ost, osh) = o.prep_init(vk, CTX, a, ap, nonces[16 * i:16 * (i + 1)], cw, ish)
+            assert chunked[0][pss * i:pss * (i + 1)] == o.test_vec_encode_prep_share(osh), "agg %d report %d" % (a, i)
+            assert chunked[2][osz * i:osz * (i + 1)] == o.field.encode_vec(ost[0]), "agg %d report %d" % (a, i)
+
+
 def test_malformed_payload_correction_word_detected(mastic_amd):
     """poc/tests/test_mastic.py:126-175: tweak a payload CW -> eval proofs differ."""
     rng = random.Random(10)
