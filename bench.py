@@ -263,7 +263,10 @@ def max_over_ranks(dist, torch, x):
 def lib_comm_init(m, dist, world, rank):
     """Join m's ctx to the library's own RCCL communicator: rank 0 creates the
     id (mastic_comm_unique_id), the gloo control group broadcasts it, every
-    rank calls mastic_comm_init (collective)."""
+    rank calls mastic_comm_init (collective).  Returns False, on every rank,
+    if any rank's init failed (the ranks agree over gloo): the agg shares then
+    merge over torch.distributed instead (stderr says so)."""
+    import torch
     from mastic_amd.merge import exchange_unique_id
 
     def bcast(obj):
@@ -271,7 +274,21 @@ def lib_comm_init(m, dist, world, rank):
         dist.broadcast_object_list(box, src=0)
         return box[0]
 
-    m.comm_init(world, rank, exchange_unique_id(m, rank, bcast))
+    ok = 1
+    try:
+        m.comm_init(world, rank, exchange_unique_id(m, rank, bcast))
+    except Exception as e:  # noqa: BLE001 -- reported, and every rank falls back together
+        print("bench.py rank %d: mastic_comm_init failed (%s)" % (rank, e), file=sys.stderr)
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return True
+    if ok:
+        m.comm_destroy()
+    print("bench.py rank %d: agg shares merge over torch.distributed (no library communicator)" % rank,
+          file=sys.stderr)
+    return False
 
 
 # ---------------------------------------------------------------- sweeps
@@ -447,8 +464,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     thresholds = {"default": threshold}
     if vr > 1:
         merge = VirtualRanksMerge(m, alphas_job[n_rep:], w_job[n_rep:])
-    elif dist and getattr(args, "lib_comm", False):
-        lib_comm_init(m, dist, world, rank)
+    elif dist and getattr(args, "lib_comm", False) and lib_comm_init(m, dist, world, rank):
         merge = CommMerge(m)
     else:
         merge = merge_field_shares(m, dist) if dist else None
@@ -933,7 +949,7 @@ def main():
     if args.memory_budget_gb:
         m.set_memory_budget(int(args.memory_budget_gb * 2 ** 30))
     if lib_comm:
-        lib_comm_init(m, dist, world, rank)
+        lib_comm = lib_comm_init(m, dist, world, rank)
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
     # distinct reports resident in HBM: all of them, or a pool the job cycles through
