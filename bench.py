@@ -566,7 +566,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     # counts a minimal evaluation), so `frac` leaves it out and
     # `frac_executed` counts it
     per_level = {"level": [], "hit": [], "candidates": [], "nodes_per_report": [], "level_kernel_ms": [],
-                 "absorb_ms": [], "frac": []}
+                 "absorb_ms": [], "frac": [], "frac_executed": []}
     rec_ops = 0
     ab_perms = 0.0  # binder-sponge Keccak-p of the first timed sweep, both aggregators
     wl_b = m.VALUE_LEN * m.field.ENCODED_SIZE
@@ -586,6 +586,9 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         per_level["absorb_ms"].append(round(timing[ti][4] + timing[ti + 1][4], 2))
         per_level["frac"].append(round(2 * n_rep * nl * dom_ops / (ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 3)
                                  if ms > 0 else None)
+        rec_l = 2 * n_rep * parents * (aes_per_node - 1) * AES_BLOCK_OPS if hit_l else 0
+        per_level["frac_executed"].append(
+            round((2 * n_rep * nl * dom_ops + rec_l) / (ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 3) if ms > 0 else None)
         if hit_l:
             rec_ops += 2 * n_rep * parents * (aes_per_node - 1) * AES_BLOCK_OPS
             # a hit absorbs its new level's proofs and level L-1's parents' differences
