@@ -260,35 +260,86 @@ def max_over_ranks(dist, torch, x):
     return float(tt.item())
 
 
-def lib_comm_init(m, dist, world, rank):
+def lib_comm_init(m, dist, world, rank, timeout_ms=0):
     """Join m's ctx to the library's own RCCL communicator: rank 0 creates the
     id (mastic_comm_unique_id), the gloo control group broadcasts it, every
-    rank calls mastic_comm_init (collective).  Returns False, on every rank,
-    if any rank's init failed (the ranks agree over gloo): the agg shares then
-    merge over torch.distributed instead (stderr says so)."""
+    rank calls mastic_comm_init_timeout (collective; a peer that never joins
+    ends in ETIMEDOUT after the library's bound instead of a hang), and the
+    ranks agree on the outcome over gloo.  There is no fallback: if any rank's
+    init failed, every rank raises SystemExit(3) (the run exits non-zero; the
+    gloo merge exists only as the MASTIC_BENCH_BACKEND=gloo rehearsal)."""
     import torch
-    from mastic_amd.merge import exchange_unique_id
 
     def bcast(obj):
         box = [obj]
         dist.broadcast_object_list(box, src=0)
         return box[0]
 
+    err = None
+    uid = None
+    if rank == 0:
+        try:
+            uid = m.comm_unique_id()
+        except Exception as e:  # noqa: BLE001 -- rank 0 could not create the id: every rank learns it
+            err = e
+    uid = bytes(bcast(uid or b""))
+    dist.barrier()  # every rank is at its init: none waits on a peer still generating data
     ok = 1
-    try:
-        m.comm_init(world, rank, exchange_unique_id(m, rank, bcast))
-    except Exception as e:  # noqa: BLE001 -- reported, and every rank falls back together
-        print("bench.py rank %d: mastic_comm_init failed (%s)" % (rank, e), file=sys.stderr)
+    if err is None and not uid:
+        err = RuntimeError("rank 0 could not create the communicator id")
+    if err is None:
+        try:
+            m.comm_init(world, rank, uid, timeout_ms)
+        except Exception as e:  # noqa: BLE001 -- reported below, on every rank
+            err = e
+    if err is not None:
         ok = 0
+        print("bench.py rank %d: mastic_comm_init failed (%s)" % (rank, err), file=sys.stderr, flush=True)
     flag = torch.tensor([ok], dtype=torch.int32)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 1:
         return True
     if ok:
         m.comm_destroy()
-    print("bench.py rank %d: agg shares merge over torch.distributed (no library communicator)" % rank,
-          file=sys.stderr)
-    return False
+    print("bench.py rank %d: a rank could not join the library's RCCL communicator; exiting (no silent fallback "
+          "to another merge path)" % rank, file=sys.stderr, flush=True)
+    raise SystemExit(3)
+
+
+def device_desc(local):
+    """This rank's GPU for the bench line's comm record."""
+    import torch
+    d = {"local_rank": local}
+    try:
+        props = torch.cuda.get_device_properties(local)
+        d["name"] = props.name
+        for k in ("pci_bus_id", "pci_device_id", "pci_domain_id", "uuid"):
+            if hasattr(props, k):
+                d[k] = str(getattr(props, k))
+    except Exception as e:  # noqa: BLE001 -- descriptive only
+        d["error"] = str(e)
+    return d
+
+
+def comm_record(dist, world, rank, lib_comm, m=None, desc=None):
+    """The merge path of a bench line: which transport carried the ranks' agg
+    shares, how many ranks the library's communicator saw, and every rank's
+    device (gathered over the control group).  desc: this rank's device
+    record (default: device_desc of LOCAL_RANK)."""
+    if desc is None:
+        desc = device_desc(int(os.environ.get("MASTIC_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0"))))
+    desc = dict(desc, rank=rank)
+    if dist is None:
+        return {"backend": "none", "nranks": 1, "devices": [desc], "path": "single process: no merge"}
+    devs = [None] * world
+    dist.all_gather_object(devs, desc)
+    if lib_comm:
+        return {"backend": "rccl", "nranks": int(m.comm_info()[0]), "devices": devs,
+                "path": "library-owned RCCL communicator: mastic_aggregate_merged / mastic_allgather_fold "
+                        "(agreement round, ncclAllGather, GF(p) fold on the GPU)"}
+    return {"backend": "gloo-rehearsal", "nranks": world, "devices": devs,
+            "path": "MASTIC_BENCH_BACKEND=gloo: host copies all-gathered over gloo, GF(p) fold on the GPU "
+                    "(ranks sharing one GPU)"}
 
 
 # ---------------------------------------------------------------- sweeps
@@ -468,6 +519,9 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
         merge = CommMerge(m)
     else:
         merge = merge_field_shares(m, dist) if dist else None
+    comm = comm_record(dist, world, rank, isinstance(merge, CommMerge), m) if vr == 1 else {
+        "backend": "none (virtual ranks)", "nranks": 1, "devices": [], "path": "VirtualRanksMerge: the other "
+        "ranks' aggregates added in plaintext"}
 
     cached_levels = []
     phases = {}
@@ -638,6 +692,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             "hbm_used_gb_after": hbm_used,
             "parallelism": "reports split %d-way, per-level agg-share all-gather + GPU fold" % world,
         },
+        "comm": comm,
         "roofline": {
             "kernel": "k_eval_aes<F64> (+ node-proof waves, + k_node_proof for the last level)",
             "bound": "valu",
@@ -953,6 +1008,7 @@ def main():
         m.set_memory_budget(int(args.memory_budget_gb * 2 ** 30))
     if lib_comm:
         lib_comm = lib_comm_init(m, dist, world, rank)
+    comm = comm_record(dist, world, rank, lib_comm, m)
     ctx = b"mastic-mi355x-bench"
     seed = 0x4D41 + int(args.config[1])
     # distinct reports resident in HBM: all of them, or a pool the job cycles through
@@ -1046,6 +1102,7 @@ def main():
             "field": "Field64" if fname == "F64" else "Field128",
             "parallelism": "reports sharded %d-way" % world,
         },
+        "comm": comm,
         "roofline": {
             "kernel": dom,
             "bound": "valu",
@@ -1248,6 +1305,7 @@ def main():
             "roofline_kernel": ns["roofline"]["kernel"],
             "per_level": ns["per_level"],
             "breakdown_ms": ns["breakdown_ms_per_step"],
+            "comm": ns["comm"],
         }
         if "cpu_baseline" in ns:
             cb = ns["cpu_baseline"]

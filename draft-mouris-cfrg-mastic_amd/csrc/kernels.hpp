@@ -1811,3 +1811,11 @@ __global__ __launch_bounds__(256) void k_accept(int n, int stride, int check_jr,
     }
     accept[r] = ok ? 1 : 0;
 }
+
+// Test hook (mastic_set_test_sponge_delay): one wave idles `ticks` periods of
+// the constant wall clock, holding the stream it is queued on, so the work a
+// prep_init queues there afterwards completes late.  No memory access.
+__global__ __launch_bounds__(64) void k_spin(unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}

@@ -5,6 +5,7 @@
 // the kernels of kernels.hpp / shard.hpp.
 #include "mastic_hip.h"
 
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -16,6 +17,8 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "host_tree.hpp"
@@ -175,7 +178,13 @@ struct mastic_ctx {
     // library-owned RCCL communicator (mastic_comm_init; none = world 1)
     ncclComm_t comm = nullptr;
     int comm_n = 1, comm_rank = 0;
+    bool comm_broken = false;  // aborted after a failed / timed-out step: collective calls fail
+    int comm_timeout_ms = MASTIC_COMM_TIMEOUT_MS;  // bound of every wait on the communicator
     DevBuf comm_local, comm_gather, comm_out;  // mastic_aggregate_merged / mastic_allgather_fold staging
+    DevBuf comm_st;                            // agreement round: this rank's status + every rank's
+    void* comm_st_host = nullptr;              // pinned host copy of the same (nranks + 1 records)
+    size_t comm_st_host_n = 0;
+    void comm_release();                       // teardown of a live communicator (defined with the RCCL binding)
     PrefixState pfx_host[PFX_COUNT];
     std::string err;
     uint64_t budget = 0;
@@ -217,6 +226,10 @@ struct mastic_ctx {
     // result-preserving test hooks (mastic_set_test_hooks; nothing in the environment sets them)
     int force_slow_blk = -1;    // exact payload stream from this block on
     int fail_allocs = 0;        // this many result / cache-slot allocations fail first (ENOMEM recovery)
+    int sponge_delay_us = 0;    // the next prep_init first holds the sponge stream this long (k_spin)
+    int wall_khz = 100000;      // wall_clock64() rate (hipDeviceAttributeWallClockRate)
+    bool timing_nowait = false; // A/B of the last_timing fix only (MASTIC_DBG_TIMING_NOWAIT, knob builds)
+    bool serial_sponges = false;  // timing only: sponge launches run alone (MASTIC_SERIAL_SPONGES, knob builds)
     bool inject_alloc_failure() {
         if (fail_allocs <= 0) return false;
         fail_allocs--;
@@ -290,7 +303,8 @@ struct mastic_ctx {
             for (auto e : x.ev) (void)hipEventDestroy(e);
         for (auto e : sync_ev) (void)hipEventDestroy(e);
         if (fold_ev) (void)hipEventDestroy(fold_ev);
-        if (comm) (void)ncclCommDestroy(comm);
+        if (comm) comm_release();
+        if (comm_st_host) (void)hipHostFree(comm_st_host);
         if (tree_ev) (void)hipEventDestroy(tree_ev);
         if (tree_stage) (void)hipHostFree(tree_stage);
         if (stream) (void)hipStreamDestroy(stream);
@@ -684,14 +698,22 @@ static int choose_eval_ppw(int n_parents, int groups, int aes_waves, int n_cus) 
 // items per wave x blocks per item.  Pick the split minimising that (each
 // item recomputes the extend pair; item 0 adds the next-seed pair), fewer
 // items on ties.  At 16 or more parents this is 1 (no split).
-static void choose_split(int n_parents, int nblk, int* split, int* split_blocks) {
+// The proof waves first compute level l-1's node proofs (2 np_prev per
+// report, spread over them; ~3 AES blocks of time per Keccak-p, the ratio
+// miss_proof_waves uses) and then claim items from the same LDS counter, so
+// the 16 waves' capacity is reduced by that head start.
+static void choose_split(int n_parents, int np_prev, int proof_waves, int nblk, int* split, int* split_blocks) {
     int best_k = 1, best_cost = 1 << 30;
+    const int pw = std::max(1, proof_waves);
+    const int proof_blocks = np_prev > 0 ? pw * ((2 * np_prev + pw - 1) / pw) * 3 : 0;
     for (int k = 1; k <= nblk; k++) {
         const int nb = (nblk + k - 1) / k;
         const int kk = (nblk + nb - 1) / nb;  // ranges actually non-empty
         if (kk != k) continue;
-        const int per_wave = (n_parents * k + EVAL_WAVES - 1) / EVAL_WAVES;
-        const int cost = per_wave * (2 + 2 * nb) + 2;
+        const int chain = 2 + 2 * nb;
+        // the items' waves: whole items per wave after the proof waves' head start
+        const int per_wave = (n_parents * k * chain + proof_blocks + EVAL_WAVES * chain - 1) / (EVAL_WAVES * chain);
+        const int cost = per_wave * chain + 2;
         if (cost < best_cost) {
             best_cost = cost;
             best_k = k;
@@ -806,8 +828,11 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         const size_t nctrl = (2 * (size_t)p.bits + 7) / 8;
         const size_t row_bytes = (size_t)(l_hi - l_lo) * (16 + (size_t)p.value_len * p.enc + 32) +
                                  (agg_id == 0 ? (size_t)p.proof_len * p.enc : 0);
+        // (grid y of every row-tile launch below: 64 words per workgroup row)
+        const size_t max_words = std::max<size_t>((size_t)p.value_len * p.w32 * (l_hi - l_lo),
+                                                  agg_id == 0 ? (size_t)p.proof_len * p.w32 : 0);
         const bool tiles = row_bytes >= 16384 && (((uintptr_t)pub | (uintptr_t)in_b | ps | is | nctrl) & 7) == 0 &&
-                           (size_t)p.value_len * p.w32 * (l_hi - l_lo) / 64 < 65535;  // grid y
+                           (max_words + 63) / 64 < 65535;
         hipLaunchKernelGGL(k_unpack, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, pl, agg_id,
                            rep->nonces.as<uint8_t>() + 16 * base, pub, in_b, l_lo, l_hi, tiles ? 1 : 0);
         if (tiles) {
@@ -825,6 +850,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             rows(seg + 32 * (size_t)l_lo, ps, 8 * nl, pl.cw_proof + (size_t)8 * l_lo * stride);
             if (agg_id == 0) rows(in_b + 16, is, p.proof_len * p.w32, pl.lps);
         }
+        HIPCHK(c, hipGetLastError());
     }
     const bool whole = base == 0 && (size_t)n == rep->n && W == c->work.p;
     const bool rk_ok = hit && whole && c->rk.valid && c->rk.rep_id == rep->id && c->rk.rep_gen == rep->generation() &&
@@ -902,6 +928,9 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipGetLastError());
         *done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(*done, as));
+        // timing experiments only (MASTIC_SERIAL_SPONGES): the main stream waits
+        // for this launch, so it runs alone on the chip (standalone sponge rate)
+        if (c->serial_sponges && as != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, *done, 0));
         if (which0 == 0) f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
         if (which0 + nwh > 1) f_pl = (f_pl + ab.nbytes[1]) % KECCAK_RATE;
         return 0;
@@ -991,7 +1020,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
             a.split_blocks = nblk;
             // (<= 32 parents: their pass-0 flags live in the workgroup's sync words)
             if (!hit && l < t->L && c->small_split && np_ <= 32 && !(c->dbg_skip & 2))
-                choose_split(np_, nblk, &a.split, &a.split_blocks);
+                choose_split(np_, l > 0 ? t->n_parents[l - 1] : 0, c->proof_waves, nblk, &a.split,
+                             &a.split_blocks);
         }
         const int n_items = np_ * a.split;
         a.ppw = choose_eval_ppw(n_items, groups, par_waves, c->n_cus);
@@ -1204,6 +1234,13 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     static const uint8_t empty_vk[1] = {0};
     if (!verify_key) verify_key = empty_vk;
     c->tcur = agg_id;
+    if (c->sponge_delay_us > 0) {
+        // test hook: the sponge stream is busy when this call records its marks there
+        const unsigned long long ticks = (unsigned long long)c->sponge_delay_us * (unsigned long long)c->wall_khz / 1000;
+        c->sponge_delay_us = 0;
+        hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, c->stream2, ticks);
+        HIPCHK(c, hipGetLastError());
+    }
     Tree* t = nullptr;
     int rc = build_tree(c, enc_agg_param, agg_param_len, &t);
     if (rc) return rc;
@@ -1625,8 +1662,10 @@ extern "C" int mastic_aggregate(mastic_ctx* c, int agg_id, const uint8_t* valid,
     return 0;
 }
 
-extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t* valid, void* dev_agg_share,
-                                       void* caller_stream) {
+// (ABI 6: the only name of this function; mastic_aggregate_device, whose
+// argument count changed between ABI 3, 4 and 5, is gone)
+extern "C" int mastic_aggregate_device_on_stream(mastic_ctx* c, int agg_id, const uint8_t* valid,
+                                                 void* dev_agg_share, void* caller_stream) {
     DeviceScope ds_(c);
     if (!c || (agg_id != 0 && agg_id != 1)) return fail(c, MASTIC_EINVAL, "invalid aggregator ID");
     Result& R = c->res[agg_id];
@@ -1643,12 +1682,6 @@ extern "C" int mastic_aggregate_device(mastic_ctx* c, int agg_id, const uint8_t*
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's stream (e.g. RCCL's) reads it next
     return 0;
-}
-
-// ABI-4 name of the same function.
-extern "C" int mastic_aggregate_device_on_stream(mastic_ctx* c, int agg_id, const uint8_t* valid,
-                                                 void* dev_agg_share, void* caller_stream) {
-    return mastic_aggregate_device(c, agg_id, valid, dev_agg_share, caller_stream);
 }
 
 extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t n_shares, size_t n_elems,
@@ -1674,30 +1707,247 @@ extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t 
 }
 
 // ---- multi-GPU merge over the ctx's own RCCL communicator --
+//
+// Failure model.  Every collective entry point (mastic_allgather_fold,
+// mastic_merge_host, mastic_aggregate_merged) first does all of its
+// rank-local work -- argument checks, staging allocations, the local fold --
+// and then joins an agreement round: one 32-byte CommStatus per rank (its
+// error code, the entry point, n_local, n_elems), all-gathered into buffers
+// sized at mastic_comm_init.  A rank whose local work failed still joins it,
+// so no peer is left waiting inside a data all-gather: a rank that failed
+// returns its own error, every other rank the code of the lowest failing
+// rank, and ranks whose calls disagree on the entry point or the share
+// geometry all return MASTIC_EINVAL, before any share bytes move.  Only when
+// every rank is ready do the data all-gather and the GF(p) fold run.  Every
+// wait on the communicator is bounded by the ctx's timeout
+// (mastic_comm_init_timeout): a peer that never joins (it crashed, or is stuck
+// elsewhere) becomes MASTIC_ETIMEDOUT, and the communicator is aborted
+// (ncclCommAbort); later collective calls then fail with MASTIC_EHIP -- never
+// a silent world-1 merge -- until mastic_comm_destroy and a new
+// mastic_comm_init.
 
-#define NCCLCHK(c, x)                                                                    \
-    do {                                                                                 \
-        const ncclResult_t r_ = (x);                                                     \
-        if (r_ != ncclSuccess) return fail((c), MASTIC_EHIP, "RCCL: %s", ncclGetErrorString(r_)); \
-    } while (0)
+namespace {
+// RCCL is bound on first use of a communicator entry point (dlopen), so a
+// single-GPU user of the library has no load-time dependency on librccl; a
+// process that already holds it (e.g. PyTorch's copy) shares that one.
+struct RcclApi {
+    bool ok = false;
+    std::string why;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
+    decltype(&ncclCommFinalize) CommFinalize = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+
+const RcclApi& rccl() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) {
+            const char* e = dlerror();
+            a.why = e ? e : "librccl.so.1 not found";
+            return a;
+        }
+        bool all = true;
+        auto bind = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn && all) a.why = std::string("librccl lacks ") + name;
+            all = all && fn;
+        };
+        bind(a.GetUniqueId, "ncclGetUniqueId");
+        bind(a.CommInitRankConfig, "ncclCommInitRankConfig");
+        bind(a.CommInitRank, "ncclCommInitRank");
+        bind(a.CommGetAsyncError, "ncclCommGetAsyncError");
+        bind(a.CommAbort, "ncclCommAbort");
+        bind(a.CommFinalize, "ncclCommFinalize");
+        bind(a.CommDestroy, "ncclCommDestroy");
+        bind(a.AllGather, "ncclAllGather");
+        bind(a.GetErrorString, "ncclGetErrorString");
+        a.ok = all;
+        return a;
+    }();
+    return api;
+}
+
+// One rank's record in the agreement round of a collective call.
+struct CommStatus {
+    int32_t rc;        // 0 = this rank's local work succeeded, else its MASTIC_E* code
+    uint32_t op;       // entry point (CommOp)
+    uint64_t n_local;  // shares per rank
+    uint64_t n_elems;  // elements per share
+    uint32_t magic;
+    uint32_t pad;
+};
+static_assert(sizeof(CommStatus) == 32, "CommStatus layout");
+constexpr uint32_t COMM_MAGIC = 0x4d415354u;
+enum CommOp : uint32_t { COMM_ALLGATHER_FOLD = 1, COMM_MERGE_HOST = 2, COMM_AGGREGATE_MERGED = 3 };
+const char* comm_op_name(uint32_t op) {
+    return op == COMM_ALLGATHER_FOLD ? "mastic_allgather_fold"
+           : op == COMM_MERGE_HOST   ? "mastic_merge_host"
+           : op == COMM_AGGREGATE_MERGED ? "mastic_aggregate_merged" : "?";
+}
+}  // namespace
+
+// ctx teardown: its queued work is waited for, then the communicator is
+// released locally (ncclCommAbort never waits on peers that may be gone).
+void mastic_ctx::comm_release() {
+    (void)hipStreamSynchronize(stream);
+    (void)rccl().CommAbort(comm);
+    comm = nullptr;
+}
+
+// Abort the ctx's communicator after a failed or timed-out RCCL step: its
+// kernels see the abort flag and exit, the ctx keeps comm_broken so later
+// collective calls fail instead of silently folding as world 1.
+static int comm_abort(mastic_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c->comm) (void)rccl().CommAbort(c->comm);
+    c->comm = nullptr;
+    c->comm_broken = true;
+    return fail(c, code, "%s; the communicator was aborted", buf);
+}
+
+// A non-blocking communicator's call may return ncclInProgress: poll its
+// state until it settles, within the ctx's timeout.
+static int comm_settle(mastic_ctx* c, ncclResult_t r, const char* what) {
+    const double t0 = now_ms();
+    while (r == ncclInProgress) {
+        if (now_ms() - t0 > c->comm_timeout_ms)
+            return comm_abort(c, MASTIC_ETIMEDOUT, "RCCL %s did not complete within %d ms", what, c->comm_timeout_ms);
+        std::this_thread::yield();
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t q = rccl().CommGetAsyncError(c->comm, &st);
+        r = q != ncclSuccess ? q : st;
+    }
+    if (r != ncclSuccess) return comm_abort(c, MASTIC_EHIP, "RCCL %s: %s", what, rccl().GetErrorString(r));
+    return 0;
+}
+
+// Wait for c->stream, which carries an RCCL collective: bounded by the ctx's
+// timeout (a peer that never joins), watching the communicator's own errors.
+static int comm_wait(mastic_ctx* c, const char* what) {
+    const double t0 = now_ms();
+    for (int spin = 0;; spin++) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) return 0;
+        if (e != hipErrorNotReady) {
+            (void)hipGetLastError();
+            return comm_abort(c, MASTIC_EHIP, "%s: %s", what, hipGetErrorString(e));
+        }
+        ncclResult_t st = ncclSuccess;
+        if (rccl().CommGetAsyncError(c->comm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+            return comm_abort(c, MASTIC_EHIP, "RCCL %s: %s", what, rccl().GetErrorString(st));
+        if (now_ms() - t0 > c->comm_timeout_ms)
+            return comm_abort(c, MASTIC_ETIMEDOUT, "%s: a peer rank did not join within %d ms", what,
+                              c->comm_timeout_ms);
+        if (spin < 2000)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+// A staging buffer of a collective call (counts against the fail_allocs
+// test hook when it must actually allocate).
+static bool comm_grow(mastic_ctx* c, DevBuf& b, size_t want) {
+    if (want <= b.bytes && b.p) return true;
+    if (c->inject_alloc_failure()) return false;
+    return b.grow(want);
+}
+
+// The agreement round (see the failure model above).  local_rc: the outcome
+// of this rank's local work (0, or a code whose text is already in c->err).
+// Returns 0 iff every rank is ready for the data exchange.
+static int comm_agree(mastic_ctx* c, int local_rc, uint32_t op, size_t n_local, size_t n_elems) {
+    if (!c->comm) {
+        if (c->comm_broken && !local_rc)
+            return fail(c, MASTIC_EHIP, "the ctx's communicator was aborted after an earlier failure "
+                                        "(mastic_comm_destroy, then mastic_comm_init)");
+        return local_rc;  // world 1
+    }
+    const std::string local_err = c->err;
+    CommStatus* h = (CommStatus*)c->comm_st_host;  // [0]: this rank's record, [1 + r]: rank r's
+    h[0] = CommStatus{local_rc, op, (uint64_t)n_local, (uint64_t)n_elems, COMM_MAGIC, 0};
+    uint8_t* d = c->comm_st.as<uint8_t>();
+    hipError_t e = hipMemcpyAsync(d, h, sizeof(CommStatus), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return comm_abort(c, local_rc ? local_rc : MASTIC_EHIP, "%s: status upload: %s", comm_op_name(op),
+                          hipGetErrorString(e));
+    }
+    int rc = comm_settle(c, rccl().AllGather(d, d + sizeof(CommStatus), sizeof(CommStatus), ncclUint8, c->comm,
+                                             c->stream), "status all-gather");
+    if (rc) return local_rc ? local_rc : rc;
+    e = hipMemcpyAsync(h + 1, d + sizeof(CommStatus), sizeof(CommStatus) * (size_t)c->comm_n, hipMemcpyDeviceToHost,
+                       c->stream);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return comm_abort(c, local_rc ? local_rc : MASTIC_EHIP, "%s: status download: %s", comm_op_name(op),
+                          hipGetErrorString(e));
+    }
+    rc = comm_wait(c, "status all-gather");
+    if (rc) return local_rc ? local_rc : rc;
+    int first_bad = -1, mismatch = -1;
+    for (int r = 0; r < c->comm_n; r++) {
+        const CommStatus& s = h[1 + r];
+        if (s.magic != COMM_MAGIC || s.op != op || s.n_local != n_local || s.n_elems != n_elems) {
+            if (mismatch < 0) mismatch = r;
+        } else if (s.rc != 0 && first_bad < 0) {
+            first_bad = r;
+        }
+    }
+    if (local_rc) {
+        c->err = local_err;
+        return local_rc;
+    }
+    if (first_bad >= 0)
+        return fail(c, h[1 + first_bad].rc, "%s failed on rank %d (code %d); no shares were exchanged",
+                    comm_op_name(op), first_bad, h[1 + first_bad].rc);
+    if (mismatch >= 0) {
+        const CommStatus& s = h[1 + mismatch];
+        return fail(c, MASTIC_EINVAL,
+                    "ranks disagree on the collective call: rank %d called %s with %llu x %llu elements, this rank "
+                    "%s with %zu x %zu; no shares were exchanged",
+                    mismatch, comm_op_name(s.op), (unsigned long long)s.n_local, (unsigned long long)s.n_elems,
+                    comm_op_name(op), n_local, n_elems);
+    }
+    return 0;
+}
+
+// Staging for the data all-gather of n_local shares of n_elems elements from
+// every rank (allocated in the local phase, before the agreement).
+static bool comm_stage_gather(mastic_ctx* c, size_t n_local, size_t n_elems) {
+    return !c->comm || comm_grow(c, c->comm_gather, std::max<size_t>(n_local * n_elems * c->p.w32 * 4, 4) * c->comm_n);
+}
 
 // dev_out = sum mod p of the n_local shares of every rank (n_elems elements
-// each), queued on c->stream: one ncclAllGather of this rank's shares into a
-// rank-ordered buffer, then k_fold_shares over the n_local x nranks shares
-// (RCCL's integer sum is not GF(p) addition).  Without a communicator the
-// local shares are folded directly (world 1).
+// each), queued on c->stream after a successful agreement: one ncclAllGather
+// of this rank's shares into the rank-ordered comm_gather, then
+// k_fold_shares over the n_local x nranks shares (RCCL's integer sum is not
+// GF(p) addition).  Without a communicator the local shares are folded
+// directly (world 1).
 static int allgather_fold_impl(mastic_ctx* c, const uint32_t* local, size_t n_local, size_t n_elems, uint32_t* out) {
     const size_t local_bytes = n_local * n_elems * c->p.w32 * 4;
     const uint32_t* src = local;
     size_t n_shares = n_local;
     if (c->comm && local_bytes) {
-        if (!c->comm_gather.grow(local_bytes * (size_t)c->comm_n)) return fail(c, MASTIC_ENOMEM, "out of device memory");
-        NCCLCHK(c, ncclAllGather(local, c->comm_gather.p, local_bytes, ncclUint8, c->comm, c->stream));
+        int rc = comm_settle(c, rccl().AllGather(local, c->comm_gather.p, local_bytes, ncclUint8, c->comm, c->stream),
+                             "share all-gather");
+        if (rc) return rc;
         src = c->comm_gather.as<uint32_t>();
         n_shares = n_local * (size_t)c->comm_n;
     }
-    if (n_shares > (size_t)INT32_MAX || n_elems > (size_t)INT32_MAX)
-        return fail(c, MASTIC_EINVAL, "too many shares to fold");
     const dim3 grid((unsigned)((n_elems + 255) / 256));
     if (c->p.field == 64)
         hipLaunchKernelGGL(k_fold_shares<F64>, grid, dim3(256), 0, c->stream, src, (int)n_shares, (int)n_elems, out);
@@ -1707,28 +1957,83 @@ static int allgather_fold_impl(mastic_ctx* c, const uint32_t* local, size_t n_lo
     return 0;
 }
 
+// The end of a collective call: its queued work (the data all-gather, the
+// fold, the copy out) done, bounded by the timeout when RCCL is in it.
+static int comm_finish(mastic_ctx* c, uint32_t op) {
+    if (c->comm) return comm_wait(c, comm_op_name(op));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Shape limits of the fold kernel (k_fold_shares takes int counts).
+static int comm_check_counts(mastic_ctx* c, size_t n_local, size_t n_elems) {
+    if (n_local * (size_t)c->comm_n > (size_t)INT32_MAX || n_elems > (size_t)INT32_MAX)
+        return fail(c, MASTIC_EINVAL, "too many shares to fold");
+    return 0;
+}
+
 extern "C" int mastic_comm_unique_id(uint8_t id_out[MASTIC_COMM_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == MASTIC_COMM_ID_BYTES, "ncclUniqueId size");
     if (!id_out) return MASTIC_EINVAL;
+    if (!rccl().ok) return MASTIC_ENODEV;
     ncclUniqueId id;
-    if (ncclGetUniqueId(&id) != ncclSuccess) return MASTIC_EHIP;
+    if (rccl().GetUniqueId(&id) != ncclSuccess) return MASTIC_EHIP;
     std::memcpy(id_out, &id, sizeof(id));
     return 0;
 }
 
-extern "C" int mastic_comm_init(mastic_ctx* c, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES]) {
+extern "C" int mastic_comm_init_timeout(mastic_ctx* c, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES],
+                                        int timeout_ms) {
     DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
     if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(c, MASTIC_EINVAL, "invalid communicator rank");
     if (c->comm) return fail(c, MASTIC_EINVAL, "the ctx already has a communicator");
+    if (!rccl().ok) return fail(c, MASTIC_ENODEV, "RCCL is not available: %s", rccl().why.c_str());
+    c->comm_timeout_ms = timeout_ms > 0 ? timeout_ms : MASTIC_COMM_TIMEOUT_MS;
+    // the agreement round's buffers, before joining: a rank that cannot
+    // allocate them fails here, before any collective
+    const size_t st_bytes = sizeof(CommStatus) * ((size_t)nranks + 1);
+    if (!c->comm_st.ensure(st_bytes)) return fail(c, MASTIC_ENOMEM, "out of device memory");
+    if (c->comm_st_host_n < (size_t)nranks + 1) {
+        if (c->comm_st_host) (void)hipHostFree(c->comm_st_host);
+        c->comm_st_host = nullptr;
+        c->comm_st_host_n = 0;
+        HIPCHK(c, hipHostMalloc(&c->comm_st_host, st_bytes, hipHostMallocDefault));
+        c->comm_st_host_n = (size_t)nranks + 1;
+    }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
+    // Non-blocking init, so a peer that never joins ends in a timeout and
+    // ncclCommAbort rather than a hang.  The config claims the 2.14 layout,
+    // whose fields every later RCCL reads (the process may hold an RCCL other
+    // than this header's, e.g. PyTorch's); an RCCL that refuses the config
+    // gets the blocking init.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.version = NCCL_VERSION(2, 14, 0);
+    cfg.blocking = 0;
     ncclComm_t comm = nullptr;
-    NCCLCHK(c, ncclCommInitRank(&comm, nranks, uid, rank));
+    ncclResult_t r = rccl().CommInitRankConfig(&comm, nranks, uid, rank, &cfg);
+    if (r == ncclInvalidArgument && !comm) r = rccl().CommInitRank(&comm, nranks, uid, rank);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (comm) (void)rccl().CommAbort(comm);
+        return fail(c, MASTIC_EHIP, "RCCL init: %s", rccl().GetErrorString(r));
+    }
     c->comm = comm;
     c->comm_n = nranks;
     c->comm_rank = rank;
+    c->comm_broken = false;
+    int rc = comm_settle(c, r, "init");
+    if (rc) {
+        c->comm_n = 1;
+        c->comm_rank = 0;
+        c->comm_broken = false;  // nothing was joined: the ctx is world 1 again
+        return rc;
+    }
     return 0;
+}
+
+extern "C" int mastic_comm_init(mastic_ctx* c, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES]) {
+    return mastic_comm_init_timeout(c, nranks, rank, id, MASTIC_COMM_TIMEOUT_MS);
 }
 
 extern "C" int mastic_comm_info(const mastic_ctx* c, int* nranks, int* rank) {
@@ -1741,48 +2046,66 @@ extern "C" int mastic_comm_info(const mastic_ctx* c, int* nranks, int* rank) {
 extern "C" int mastic_comm_destroy(mastic_ctx* c) {
     DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
+    int rc = 0;
     if (c->comm) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        NCCLCHK(c, ncclCommDestroy(c->comm));
+        rc = comm_wait(c, "mastic_comm_destroy");
+        if (!rc) rc = comm_settle(c, rccl().CommFinalize(c->comm), "finalize");
+        if (!rc) {
+            const ncclResult_t r = rccl().CommDestroy(c->comm);
+            if (r != ncclSuccess) rc = fail(c, MASTIC_EHIP, "RCCL destroy: %s", rccl().GetErrorString(r));
+        }
     }
     c->comm = nullptr;
     c->comm_n = 1;
     c->comm_rank = 0;
-    return 0;
+    c->comm_broken = false;
+    return rc;
 }
 
 extern "C" int mastic_allgather_fold(mastic_ctx* c, const void* dev_local, size_t n_local, size_t n_elems,
                                      void* dev_out, void* caller_stream) {
     DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
-    if (n_elems && (!dev_out || (n_local && !dev_local))) return fail(c, MASTIC_EINVAL, "null share buffer");
-    if (n_elems == 0) return 0;
-    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
-    HIPCHK(c, hipEventRecord(c->fold_ev, (hipStream_t)caller_stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->fold_ev, 0));
-    int rc = allgather_fold_impl(c, (const uint32_t*)dev_local, n_local, n_elems, (uint32_t*)dev_out);
+    int rc = 0;
+    if (n_elems && (!dev_out || (n_local && !dev_local))) rc = fail(c, MASTIC_EINVAL, "null share buffer");
+    if (!rc) rc = comm_check_counts(c, n_local, n_elems);
+    if (!rc && n_elems && !comm_stage_gather(c, n_local, n_elems)) rc = fail(c, MASTIC_ENOMEM, "out of device memory");
+    if (!rc && n_elems) {
+        if (!c->fold_ev && hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming) != hipSuccess)
+            rc = fail(c, MASTIC_EHIP, "hipEventCreateWithFlags failed");
+        if (!rc && (hipEventRecord(c->fold_ev, (hipStream_t)caller_stream) != hipSuccess ||
+                    hipStreamWaitEvent(c->stream, c->fold_ev, 0) != hipSuccess))
+            rc = fail(c, MASTIC_EHIP, "ordering after the caller's stream failed");
+    }
+    rc = comm_agree(c, rc, COMM_ALLGATHER_FOLD, n_local, n_elems);
+    if (rc || n_elems == 0) return rc;
+    rc = allgather_fold_impl(c, (const uint32_t*)dev_local, n_local, n_elems, (uint32_t*)dev_out);
     if (rc) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return comm_finish(c, COMM_ALLGATHER_FOLD);
 }
 
 extern "C" int mastic_merge_host(mastic_ctx* c, const uint8_t* host_local, size_t n_local, size_t n_elems,
                                  uint8_t* host_out) {
     DeviceScope ds_(c);
     if (!c) return MASTIC_EINVAL;
-    if (n_elems && (!host_out || (n_local && !host_local))) return fail(c, MASTIC_EINVAL, "null share buffer");
-    if (n_elems == 0) return 0;
     const size_t ebytes = (size_t)c->p.w32 * 4;
-    if (!c->comm_local.grow(std::max<size_t>(n_local, 1) * n_elems * ebytes) || !c->comm_out.grow(n_elems * ebytes))
-        return fail(c, MASTIC_ENOMEM, "out of device memory");
-    if (n_local)
-        HIPCHK(c, hipMemcpyAsync(c->comm_local.p, host_local, n_local * n_elems * ebytes, hipMemcpyHostToDevice,
-                                 c->stream));
-    int rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
+    int rc = 0;
+    if (n_elems && (!host_out || (n_local && !host_local))) rc = fail(c, MASTIC_EINVAL, "null share buffer");
+    if (!rc) rc = comm_check_counts(c, n_local, n_elems);
+    if (!rc && n_elems &&
+        (!comm_grow(c, c->comm_local, std::max<size_t>(n_local, 1) * n_elems * ebytes) ||
+         !comm_grow(c, c->comm_out, n_elems * ebytes) || !comm_stage_gather(c, n_local, n_elems)))
+        rc = fail(c, MASTIC_ENOMEM, "out of device memory");
+    if (!rc && n_elems && n_local &&
+        hipMemcpyAsync(c->comm_local.p, host_local, n_local * n_elems * ebytes, hipMemcpyHostToDevice, c->stream) !=
+            hipSuccess)
+        rc = fail(c, MASTIC_EHIP, "share upload failed");
+    rc = comm_agree(c, rc, COMM_MERGE_HOST, n_local, n_elems);
+    if (rc || n_elems == 0) return rc;
+    rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(host_out, c->comm_out.p, n_elems * ebytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return comm_finish(c, COMM_MERGE_HOST);
 }
 
 extern "C" int mastic_aggregate_merged(mastic_ctx* c, uint32_t agg_mask, const uint8_t* valid, size_t n_elems,
@@ -1791,33 +2114,39 @@ extern "C" int mastic_aggregate_merged(mastic_ctx* c, uint32_t agg_mask, const u
     if (!c) return MASTIC_EINVAL;
     const bool zeros = (agg_mask & MASTIC_MERGE_ZEROS) != 0;
     agg_mask &= ~MASTIC_MERGE_ZEROS;
-    if (agg_mask == 0 || agg_mask > 3) return fail(c, MASTIC_EINVAL, "invalid aggregator mask");
-    if (n_elems && !agg_out) return fail(c, MASTIC_EINVAL, "null agg share buffer");
-    if (n_elems == 0) return 0;
     const size_t ebytes = (size_t)c->p.w32 * 4;
     const size_t n_local = (agg_mask & 1) + ((agg_mask >> 1) & 1);
-    if (!c->comm_local.grow(n_local * n_elems * ebytes) || !c->comm_out.grow(n_elems * ebytes))
-        return fail(c, MASTIC_ENOMEM, "out of device memory");
+    int rc = 0;
+    if (agg_mask == 0 || agg_mask > 3) rc = fail(c, MASTIC_EINVAL, "invalid aggregator mask");
+    if (!rc && n_elems && !agg_out) rc = fail(c, MASTIC_EINVAL, "null agg share buffer");
+    if (!rc) rc = comm_check_counts(c, n_local, n_elems);
+    for (int a = 0; a < 2 && !rc && n_elems && !zeros; a++) {
+        if (!((agg_mask >> a) & 1)) continue;
+        const Result& R = c->res[a];
+        if (!R.ready)
+            rc = fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
+        else if ((size_t)R.n_prefixes * (1 + c->p.output_len) != n_elems)
+            rc = fail(c, MASTIC_EINVAL, "agg share length does not match the last prep_init");
+    }
+    if (!rc && n_elems &&
+        (!comm_grow(c, c->comm_local, n_local * n_elems * ebytes) || !comm_grow(c, c->comm_out, n_elems * ebytes) ||
+         !comm_stage_gather(c, n_local, n_elems)))
+        rc = fail(c, MASTIC_ENOMEM, "out of device memory");
     size_t k = 0;
-    for (int a = 0; a < 2; a++) {
+    for (int a = 0; a < 2 && !rc && n_elems; a++) {
         if (!((agg_mask >> a) & 1)) continue;
         uint32_t* dst = (uint32_t*)((uint8_t*)c->comm_local.p + k++ * n_elems * ebytes);
-        const Result& R = c->res[a];
-        if (!zeros) {
-            if (!R.ready) return fail(c, MASTIC_EINVAL, "no prep_init result for this aggregator");
-            if ((size_t)R.n_prefixes * (1 + c->p.output_len) != n_elems)
-                return fail(c, MASTIC_EINVAL, "agg share length does not match the last prep_init");
-            int rc = aggregate_impl(c, a, valid, dst);
-            if (rc) return rc;
-        } else {  // this rank holds no reports for the aggregator: agg_init's zeros
-            HIPCHK(c, hipMemsetAsync(dst, 0, n_elems * ebytes, c->stream));
-        }
+        if (!zeros)
+            rc = aggregate_impl(c, a, valid, dst);
+        else if (hipMemsetAsync(dst, 0, n_elems * ebytes, c->stream) != hipSuccess)  // no reports here: agg_init's zeros
+            rc = fail(c, MASTIC_EHIP, "hipMemsetAsync failed");
     }
-    int rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
+    rc = comm_agree(c, rc, COMM_AGGREGATE_MERGED, n_local, n_elems);
+    if (rc || n_elems == 0) return rc;
+    rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(agg_out, c->comm_out.p, n_elems * ebytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return comm_finish(c, COMM_AGGREGATE_MERGED);
 }
 
 // Eval-proof Merkle tree (proof-aggregation mode, kernels.hpp k_proof_tree_*)
@@ -1878,7 +2207,8 @@ extern "C" int mastic_last_timing3(mastic_ctx* c, double* aes_ms, int* aes_launc
         // on the sponge stream while its sponges run on the main stream):
         // wait for the marks themselves (an unwaited mark gave "device not
         // ready" in a 4-rank run sharing one GPU)
-        for (int i = 0; i < -c->tm[c->tcur].n_eval; i++) HIPCHK(c, hipEventSynchronize(c->tm[c->tcur].ev[i]));
+        if (!c->timing_nowait)
+            for (int i = 0; i < -c->tm[c->tcur].n_eval; i++) HIPCHK(c, hipEventSynchronize(c->tm[c->tcur].ev[i]));
         // events: [t0, t1] then per level [aes0, aes1, proof0, proof1, absorb0, absorb1]
         const size_t evi = (size_t)(-c->tm[c->tcur].n_eval);
         double ta = 0, tp = 0, tb = 0;
@@ -2202,6 +2532,11 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
     c->p = p;
     c->device = up->device;
     c->n_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, up->device) == hipSuccess && khz > 0)
+            c->wall_khz = khz;
+    }
 #ifdef MASTIC_EXPERIMENT_KNOBS
     // A/B and timing experiments only (tools/ab_*.sh build the library with
     // -DMASTIC_EXPERIMENT_KNOBS; the shipped library reads none of these).
@@ -2255,6 +2590,10 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         if (ham) c->hit_absorb_main = ham[0] != '0';
         const char* ssp = getenv("MASTIC_SMALL_SPLIT");
         if (ssp) c->small_split = ssp[0] != '0';
+        const char* tnw = getenv("MASTIC_DBG_TIMING_NOWAIT");  // the round-5 last_timing bug, for its test's A/B
+        if (tnw) c->timing_nowait = tnw[0] == '1';
+        const char* ssr = getenv("MASTIC_SERIAL_SPONGES");
+        if (ssr) c->serial_sponges = ssr[0] == '1';
     }
 #endif
     // the level kernel's LDS (table + key schedules) is dynamic, above the
@@ -2344,6 +2683,12 @@ extern "C" int mastic_set_test_hooks(mastic_ctx* c, int force_slow_blk, int fail
     c->force_slow_blk = force_slow_blk < 0 ? -1 : force_slow_blk;
     c->fail_allocs = std::max(0, fail_allocs);
     return pending;
+}
+
+extern "C" int mastic_set_test_sponge_delay(mastic_ctx* c, int delay_us) {
+    if (!c || delay_us < 0 || delay_us > 10000000) return MASTIC_EINVAL;
+    c->sponge_delay_us = delay_us;
+    return 0;
 }
 
 extern "C" int mastic_abi_version(void) { return MASTIC_ABI_VERSION; }

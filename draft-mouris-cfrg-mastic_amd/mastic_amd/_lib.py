@@ -18,10 +18,10 @@ LIB_PATH = os.path.join(PKG_DIR, "libmastic_hip.so")
 # The library lib() loads: always the shipped in-tree build, unless an A/B tool
 # calls load(path) explicitly (no process variable can swap it).
 LOAD_PATH = LIB_PATH
-ABI_VERSION = 5  # include/mastic_hip.h MASTIC_ABI_VERSION
+ABI_VERSION = 6  # include/mastic_hip.h MASTIC_ABI_VERSION
 
 MASTIC_OK = 0
-ERRORS = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -5: "EHIP"}
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -5: "EHIP", -110: "ETIMEDOUT"}
 
 # Every symbol include/mastic_hip.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
@@ -32,13 +32,15 @@ EXPORTS = [
     "mastic_synchronize", "mastic_prep_init_batch", "mastic_decide_batch",
     "mastic_shard_batch", "mastic_last_timing", "mastic_tree_stats", "mastic_fold_shares",
     "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
-    "mastic_aggregate_device", "mastic_reports_view", "mastic_decide_results",
+    "mastic_reports_view", "mastic_decide_results",
     "mastic_aggregate_device_on_stream", "mastic_abi_version", "mastic_set_test_hooks",
-    "mastic_comm_unique_id", "mastic_comm_init", "mastic_comm_info", "mastic_comm_destroy",
+    "mastic_set_test_sponge_delay",
+    "mastic_comm_unique_id", "mastic_comm_init", "mastic_comm_init_timeout", "mastic_comm_info",
+    "mastic_comm_destroy",
     "mastic_allgather_fold", "mastic_aggregate_merged", "mastic_merge_host",
 ]
 COMM_ID_BYTES = 128  # MASTIC_COMM_ID_BYTES (= RCCL's NCCL_UNIQUE_ID_BYTES)
-ROCM_PATH = "/opt/rocm"  # librccl.so (the image's ROCm)
+ROCM_PATH = "/opt/rocm"  # the image's ROCm (the library dlopens librccl.so.1 from its lib/ on first comm use)
 
 
 class MasticParams(ctypes.Structure):
@@ -84,7 +86,7 @@ def build(verbose=False, force=False, out=None, defines=()) -> str:
     rocm_lib = os.path.join(ROCM_PATH, "lib")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I" + INCLUDE] + ["-D" + d for d in defines] + ["-o", tmp, os.path.join(CSRC, "mastic_hip.hip"),
-                                                         "-L" + rocm_lib, "-Wl,-rpath," + rocm_lib, "-lrccl"]
+                                                         "-Wl,-rpath," + rocm_lib]
     if verbose:
         print(" ".join(cmd))
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -144,9 +146,9 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_double)]),
                     "mastic_fold_shares": (i32, [P, P, sz, sz, P, P]),
-                    "mastic_aggregate_device": (i32, [P, i32, P, P, P]),
                     "mastic_comm_unique_id": (i32, [P]),
                     "mastic_comm_init": (i32, [P, i32, i32, P]),
+                    "mastic_comm_init_timeout": (i32, [P, i32, i32, P, i32]),
                     "mastic_comm_info": (i32, [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
                     "mastic_comm_destroy": (i32, [P]),
                     "mastic_allgather_fold": (i32, [P, P, sz, sz, P, P]),
@@ -155,6 +157,7 @@ def lib():
                     "mastic_aggregate_device_on_stream": (i32, [P, i32, P, P, P]),
                     "mastic_abi_version": (i32, []),
                     "mastic_set_test_hooks": (i32, [P, i32, i32]),
+                    "mastic_set_test_sponge_delay": (i32, [P, i32]),
                     "mastic_reports_view": (i32, [P, sz, sz, ctypes.POINTER(P)]),
                     "mastic_decide_results": (i32, [P, u8p, sz, P, P]),
                     "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3

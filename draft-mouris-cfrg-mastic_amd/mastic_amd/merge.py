@@ -93,7 +93,7 @@ def fold_on_gpu(m, shares, n_shares, n_elems):
 
 def aggregate_to_tensor(m, agg_id, n_elems, valid=None, out=None):
     """The GPU fold of agg_id's last prep_init out shares, left in HBM as a
-    uint8 tensor (``mastic_aggregate_device``).  The library orders the fold
+    uint8 tensor (``mastic_aggregate_device_on_stream``).  The library orders the fold
     after the work queued on torch's current stream (the tensor's allocation
     or fill) by an event."""
     import numpy as np
@@ -101,10 +101,10 @@ def aggregate_to_tensor(m, agg_id, n_elems, valid=None, out=None):
     if out is None:
         out = torch.empty(n_elems * m.field.ENCODED_SIZE, dtype=torch.uint8, device="cuda")
     v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-    rc = _lib.lib().mastic_aggregate_device(m._ctx, agg_id, _lib.buf(v),
+    rc = _lib.lib().mastic_aggregate_device_on_stream(m._ctx, agg_id, _lib.buf(v),
                                                       ctypes.c_void_p(out.data_ptr()), _current_stream_handle())
     if rc != 0:
-        raise _lib.MasticError(rc, "mastic_aggregate_device failed")
+        raise _lib.MasticError(rc, "mastic_aggregate_device_on_stream failed")
     return out
 
 
@@ -146,7 +146,7 @@ class SweepMerge:
             return b""
         if have_results:
             # k_fold writes every element; the fold is ordered after this
-            # allocation's stream by an event (mastic_aggregate_device)
+            # allocation's stream by an event (mastic_aggregate_device_on_stream)
             local = torch.empty(2 * n_elems * enc, dtype=torch.uint8, device="cuda")
             for agg_id in range(2):
                 aggregate_to_tensor(m, agg_id, n_elems, valid, out=local[agg_id * n_elems * enc:])

@@ -236,12 +236,12 @@ class Mastic:
         _check(self._ctx, _lib.lib().mastic_prep_result(self._ctx, agg_id, None, None, None, None))
 
     def aggregate_to(self, agg_id: int, valid, dev_ptr: int, stream: int = 0):
-        """``mastic_aggregate_device``: fold into caller-owned device memory
+        """``mastic_aggregate_device_on_stream``: fold into caller-owned device memory
         (e.g. a torch tensor's ``data_ptr()``); the share stays in HBM.
         ``stream`` is the hipStream_t handle whose queued work last touched
         the buffer (0 = the null stream)."""
         v = None if valid is None else np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
-        _check(self._ctx, _lib.lib().mastic_aggregate_device(
+        _check(self._ctx, _lib.lib().mastic_aggregate_device_on_stream(
             self._ctx, agg_id, _lib.buf(v), ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None)))
 
     # ------------------------------- multi-GPU merge (library-owned RCCL)
@@ -255,12 +255,16 @@ class Mastic:
             raise _lib.MasticError(rc, "mastic_comm_unique_id failed")
         return buf.raw
 
-    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
-        """``mastic_comm_init``: join this ctx to an RCCL communicator of
-        ``nranks`` GPUs (collective; one process per GPU)."""
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes, timeout_ms: int = 0):
+        """``mastic_comm_init_timeout``: join this ctx to an RCCL communicator
+        of ``nranks`` GPUs (collective; one process per GPU).  ``timeout_ms``
+        bounds the init and every later wait on the communicator (0: the
+        library's default, MASTIC_COMM_TIMEOUT_MS); a peer that does not join
+        in time raises MasticError (ETIMEDOUT) instead of hanging."""
         if len(unique_id) != _lib.COMM_ID_BYTES:
             raise ValueError("communicator id has incorrect length")
-        _check(self._ctx, _lib.lib().mastic_comm_init(self._ctx, nranks, rank, _lib.buf(bytes(unique_id))))
+        _check(self._ctx, _lib.lib().mastic_comm_init_timeout(self._ctx, nranks, rank, _lib.buf(bytes(unique_id)),
+                                                              int(timeout_ms)))
 
     def comm_info(self):
         """(nranks, rank) of the ctx's communicator ((1, 0) without one)."""
@@ -398,6 +402,12 @@ class Mastic:
         if rc < 0:
             _check(self._ctx, rc)
         return rc
+
+    def set_test_sponge_delay(self, delay_us: int):
+        """Test hook (``mastic_set_test_sponge_delay``): the next prep_init
+        first holds the binder-sponge stream for ``delay_us`` microseconds,
+        so its timing marks there complete late.  Results are unaffected."""
+        _check(self._ctx, _lib.lib().mastic_set_test_sponge_delay(self._ctx, int(delay_us)))
 
     def set_frontier_cache(self, on: bool):
         """Keep each prep_init's per-level binder inputs and last frontier in HBM so

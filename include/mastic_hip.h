@@ -47,14 +47,22 @@ extern "C" {
  * 5: mastic_aggregate_device takes the caller's stream again (its round-3,
  *    pre-versioning signature; ABI 4 had briefly dropped it), the
  *    library-owned RCCL communicator (mastic_comm_*, mastic_allgather_fold,
- *    mastic_aggregate_merged). */
-#define MASTIC_ABI_VERSION 5
+ *    mastic_aggregate_merged).
+ * 6: collective-safe merges (an agreement round before any share moves,
+ *    bounded waits, MASTIC_ETIMEDOUT), mastic_comm_init_timeout, RCCL bound at
+ *    run time (no load-time librccl dependency); the old entry point
+ *    mastic_aggregate_device is removed -- its argument count changed
+ *    between ABI 3, 4 and 5 -- and the stream form is
+ *    mastic_aggregate_device_on_stream only, so a binary built against an
+ *    older header fails to link instead of passing a garbage stream. */
+#define MASTIC_ABI_VERSION 6
 
 #define MASTIC_OK 0
 #define MASTIC_EINVAL (-22)
 #define MASTIC_ENOMEM (-12)
 #define MASTIC_ENODEV (-19)
 #define MASTIC_EHIP (-5)
+#define MASTIC_ETIMEDOUT (-110) /* a peer rank did not join a collective step in time */
 
 /* circuit ids = low byte of the reference's algorithm IDs (mastic.py:568-611) */
 #define MASTIC_COUNT 1            /* MasticCount(bits)                         */
@@ -155,10 +163,7 @@ int mastic_aggregate(mastic_ctx* ctx, int agg_id, const uint8_t* valid, uint8_t*
  * leaves HBM.  caller_stream is the hipStream_t whose queued work last
  * touched the buffer (e.g. the stream it was allocated or zero-filled on;
  * NULL = the null stream): the fold is ordered after that work by an event.
- * Returns when the buffer is written.  mastic_aggregate_device_on_stream is
- * the same function under its ABI-4 name. */
-int mastic_aggregate_device(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
-                            void* caller_stream);
+ * Returns when the buffer is written. */
 int mastic_aggregate_device_on_stream(mastic_ctx* ctx, int agg_id, const uint8_t* valid, void* dev_agg_share,
                                       void* caller_stream);
 /* Multi-GPU merge (Mastic.merge, mastic.py:390-397) of n_shares agg shares
@@ -177,11 +182,31 @@ int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares,
  * Replaces Mastic.merge (mastic.py:390-397) of the ranks' agg shares.
  * Rank 0 calls mastic_comm_unique_id and hands the id to every rank by any
  * channel it likes (a file, a socket, a launcher's store); each rank then
- * calls mastic_comm_init on its ctx (collective: blocks until all nranks
- * ranks have joined).  A ctx without a communicator behaves as world 1. */
+ * calls mastic_comm_init on its ctx (collective: returns when all nranks
+ * ranks have joined).  A ctx without a communicator behaves as world 1.
+ * librccl is loaded on the first call of this group (MASTIC_ENODEV if it
+ * cannot be).
+ *
+ * Failure model of every collective call below (mastic_allgather_fold,
+ * mastic_merge_host, mastic_aggregate_merged): each rank first does its local
+ * work (argument checks, staging allocations, the local fold), then all ranks
+ * exchange a status record; a rank whose local work failed still takes part.
+ * If any rank failed, no share bytes move: a failing rank returns its own
+ * error, every other rank the code of the lowest failing rank; calls that
+ * disagree on the entry point, n_local or n_elems return MASTIC_EINVAL on
+ * every rank.  Every wait on the communicator (init included) is bounded by
+ * the ctx's timeout: a peer that never joins yields MASTIC_ETIMEDOUT, and the
+ * communicator is then aborted -- later collective calls fail with
+ * MASTIC_EHIP (never a silent world-1 merge) until mastic_comm_destroy and a
+ * new mastic_comm_init. */
 #define MASTIC_COMM_ID_BYTES 128
+#define MASTIC_COMM_TIMEOUT_MS 120000 /* mastic_comm_init's bound on every communicator wait */
 int mastic_comm_unique_id(uint8_t id_out[MASTIC_COMM_ID_BYTES]);
 int mastic_comm_init(mastic_ctx* ctx, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES]);
+/* mastic_comm_init with the bound (ms, > 0; <= 0: MASTIC_COMM_TIMEOUT_MS) on
+ * the init itself and on every later wait on this communicator. */
+int mastic_comm_init_timeout(mastic_ctx* ctx, int nranks, int rank, const uint8_t id[MASTIC_COMM_ID_BYTES],
+                             int timeout_ms);
 /* Number of ranks / this rank of the ctx's communicator (1 / 0 without one). */
 int mastic_comm_info(const mastic_ctx* ctx, int* nranks, int* rank);
 int mastic_comm_destroy(mastic_ctx* ctx);
@@ -249,10 +274,17 @@ int mastic_abi_version(void);
  * which random data reaches with probability ~2^-32 per candidate; -1 off.
  * fail_allocs: the next that many result-buffer / frontier-cache-slot
  * allocations fail as if HBM were exhausted, driving the recovery path (wait
- * for the ctx's streams, free retired buffers and the work arena, retry).
+ * for the ctx's streams, free retired buffers and the work arena, retry); a
+ * collective call's staging allocations fail the same way (that call then
+ * returns MASTIC_ENOMEM on every rank, after the agreement round).
  * Outputs are identical either way.  Returns the number of injected failures
  * the previous setting still had pending (>= 0), or MASTIC_EINVAL. */
 int mastic_set_test_hooks(mastic_ctx* ctx, int force_slow_blk, int fail_allocs);
+/* Test hook: the next mastic_prep_init first queues a kernel that idles
+ * delay_us microseconds (0..10^7) on the ctx's binder-sponge stream, so the
+ * timing marks that call records there complete late (mastic_last_timing*
+ * must wait for them).  Results are unaffected. */
+int mastic_set_test_sponge_delay(mastic_ctx* ctx, int delay_us);
 
 /* One-shot host-buffer form of upload + prep_init + prep_result. */
 int mastic_prep_init_batch(mastic_ctx* ctx, const uint8_t* verify_key, size_t verify_key_len,

@@ -24,7 +24,7 @@ examples.py:49-74 through it on every golden vector.
 """
 import ctypes
 
-ABI_VERSION = 5  # include/mastic_hip.h MASTIC_ABI_VERSION
+ABI_VERSION = 6  # include/mastic_hip.h MASTIC_ABI_VERSION
 _EINVAL = -22
 PROOF_SIZE = 32  # mastic.py:31 (eval proofs, joint-rand parts and seeds)
 # mastic_decide_batch's per-report codes (include/mastic_hip.h)

@@ -116,3 +116,97 @@ def test_sweep_through_comm_merge_equals_local_sweep(torch_cuda):
     compute_heavy_hitters(m, ctx, {"default": 60}, reps, verify_key=vk, trace=t_comm, merge=CommMerge(m))
     assert [(lv.level, lv.prefixes, lv.agg_result) for lv in t_comm] == \
         [(lv.level, lv.prefixes, lv.agg_result) for lv in t_local]
+
+
+def _two_agg_results(m, rng, ctx, n=70):
+    """Both aggregators' prep_init of n random Mastic(6, Sum 9) reports."""
+    alphas = [tuple(bool(rng.getrandbits(1)) for _ in range(6)) for _ in range(n)]
+    weights = [rng.randrange(10) for _ in range(n)]
+    nonces = b"".join(bytes([i]) * 16 for i in range(n))
+    (pub, in0, in1) = m.shard_batch(ctx, alphas, weights, nonces, rng.randbytes(m.RAND_SIZE * n))
+    reps = m.reports_upload(nonces, pub, in0, in1)
+    cand = tuple(sorted(set(a[:4] for a in alphas)))
+    ap = (3, cand, False)
+    for a in range(2):
+        m.prep_init_device(reps, bytes(range(16)), ctx, a, ap)
+    return reps, ap, len(cand) * (1 + m.OUTPUT_LEN)
+
+
+def test_collective_local_failure_returns_cleanly(torch_cuda):
+    """A rank-local failure inside a collective call (an injected ENOMEM on a
+    staging buffer) is reported after the agreement round and leaves the
+    communicator usable: the next call merges correctly.  At world 1 the
+    agreement round is this rank alone; the same code path at N ranks makes
+    every peer return the failing rank's code instead of blocking in the
+    all-gather (include/mastic_hip.h, failure model)."""
+    import mastic_amd
+    from mastic_amd._lib import MasticError
+    torch = torch_cuda
+    rng = random.Random(61)
+    m = mastic_amd.Mastic(6, "Sum", max_measurement=9)
+    m.comm_init(1, 0, m.comm_unique_id(), timeout_ms=20000)
+    (_reps, ap, n_el) = _two_agg_results(m, rng, b"comm-enomem")
+    want = m.aggregate_device(0, ap, raw=True)
+    # fresh ctx: the first merge must allocate its staging buffers
+    m.set_test_hooks(fail_allocs=1)
+    with pytest.raises(MasticError) as ei:
+        m.aggregate_merged((0,), n_el)
+    assert ei.value.code == -12
+    assert m.set_test_hooks(fail_allocs=0) == 0  # the injected failure was used
+    assert m.aggregate_merged((0,), n_el) == want
+    # the device-buffer form: a larger share forces a new gather buffer
+    n_big = 4 * n_el + 1000
+    dev = torch.zeros(3 * n_big * 8, dtype=torch.uint8, device="cuda")
+    out = torch.empty(n_big * 8, dtype=torch.uint8, device="cuda")
+    m.set_test_hooks(fail_allocs=1)
+    with pytest.raises(MasticError) as ei:
+        m.allgather_fold(dev.data_ptr(), 3, n_big, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert ei.value.code == -12
+    m.set_test_hooks(fail_allocs=0)
+    m.allgather_fold(dev.data_ptr(), 3, n_big, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert not out.any().item()
+    # argument errors are agreed on too, and leave the communicator usable
+    with pytest.raises(ValueError):
+        m.aggregate_merged((0,), n_el + 1)
+    assert m.aggregate_merged((0, 1), 0) == b""
+    assert m.aggregate_merged((0,), n_el) == want
+    assert m.comm_info() == (1, 0)
+    m.comm_destroy()
+
+
+_TIMEOUT_SCRIPT = r"""
+import sys, time
+sys.path.insert(0, %(pkg)r)
+import mastic_amd
+from mastic_amd._lib import MasticError
+m = mastic_amd.Mastic(6, "Sum", max_measurement=9)
+t0 = time.time()
+try:
+    m.comm_init(2, 0, m.comm_unique_id(), timeout_ms=3000)   # rank 1 never joins
+    print("RESULT joined")
+except MasticError as e:
+    print("RESULT code=%%d after=%%.1f msg=%%s" %% (e.code, time.time() - t0, e))
+print("INFO", m.comm_info())
+m.comm_init(1, 0, m.comm_unique_id(), timeout_ms=3000)     # the ctx is usable again
+print("INFO2", m.comm_info(), m.merge_host(bytes(16), 2, 1).hex())
+"""
+
+
+def test_comm_init_without_peers_times_out(torch_cuda):
+    """mastic_comm_init for 2 ranks with no second rank: the non-blocking init
+    is abandoned after the ctx's timeout (ncclCommAbort) and returns
+    MASTIC_ETIMEDOUT instead of blocking forever; the ctx is world 1 again and
+    can join another communicator.  Runs in its own process, bounded."""
+    import subprocess
+    import sys
+    from conftest import PKG_ROOT
+    r = subprocess.run([sys.executable, "-c", _TIMEOUT_SCRIPT % {"pkg": PKG_ROOT}], capture_output=True, text=True,
+                       timeout=150)
+    out = r.stdout
+    assert r.returncode == 0, out + r.stderr[-3000:]
+    line = [ln for ln in out.splitlines() if ln.startswith("RESULT")][0]
+    assert "code=-110" in line, out
+    after = float(line.split("after=")[1].split()[0])
+    assert 2.5 <= after < 60, line
+    assert "INFO (1, 0)" in out
+    assert "INFO2 (1, 0) " + "00" * 8 in out

@@ -159,3 +159,35 @@ def test_queued_hits_timing_and_sync(mastic_amd):
         assert t[-1] > 0 and np.isfinite(t[-1])
     finally:
         m.set_frontier_cache(False)
+
+
+def test_hit_timing_with_busy_sponge_stream(mastic_amd):
+    """A single-chunk frontier-cache hit records empty timing marks on the
+    binder-sponge stream while its sponges run on the main stream, so the main
+    stream never waits for them.  With that stream held busy (the sponge-delay
+    test hook: a 400 ms idle kernel queued there first), mastic_last_timing3
+    right after the call -- no synchronize -- must wait for the marks
+    themselves and return finite times (round 5's "device not ready" failure
+    in a 4-rank run sharing one GPU; fixed in 47221e6).  The knob build's
+    MASTIC_DBG_TIMING_NOWAIT=1 restores the old behaviour: tools/timing_fix_ab.py."""
+    rng = random.Random(95)
+    m = mastic_amd.MasticCount(8)
+    n = 128
+    (alphas, weights, nonces, rands) = _reports(m, rng, n, 5)
+    (pub, in0, in1) = m.shard_batch(CTX, alphas, weights, nonces, rands)
+    dev = m.reports_upload(nonces, pub, in0, in1)
+    vk = bytes(16)
+    m.set_frontier_cache(True)
+    try:
+        lvl0 = (0, ((False,), (True,)), False)
+        lvl1 = (1, ((False, False), (False, True), (True, False), (True, True)), False)
+        m.prep_init_device(dev, vk, CTX, 0, lvl0)
+        m.synchronize()
+        m.set_test_sponge_delay(400000)
+        m.prep_init_device(dev, vk, CTX, 0, lvl1)
+        assert m.last_prep_was_cached()
+        t = m.last_timing3()
+        assert all(np.isfinite(x) and x >= 0 for x in t)
+        assert t[-1] > 0
+    finally:
+        m.set_frontier_cache(False)

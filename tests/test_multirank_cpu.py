@@ -116,61 +116,3 @@ def test_sweep_over_two_ranks_matches_whole_batch():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got[0] == got[1] == want
-
-
-class _FakeCommMastic:
-    """Stands in for mastic_amd.Mastic in bench.lib_comm_init: comm_init fails
-    on the ranks listed in ``fail``."""
-
-    def __init__(self, rank, fail):
-        self.rank, self.fail = rank, fail
-        self.joined = self.destroyed = False
-
-    def comm_unique_id(self):
-        return bytes(128)
-
-    def comm_init(self, nranks, rank, uid):
-        assert len(uid) == 128 and nranks == 2
-        if rank in self.fail:
-            raise RuntimeError("simulated RCCL init failure")
-        self.joined = True
-
-    def comm_destroy(self):
-        self.destroyed = True
-
-
-def _comm_worker(rank, world, port, fail, out_q):
-    import sys
-    sys.path.insert(0, ROOT)
-    sys.path.insert(0, PKG_ROOT)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench
-    m = _FakeCommMastic(rank, fail)
-    ok = bench.lib_comm_init(m, dist, world, rank)
-    out_q.put((rank, ok, m.joined, m.destroyed))
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("fail", [(), (1,), (0, 1)], ids=["none", "rank1", "both"])
-def test_bench_comm_init_ranks_agree(fail):
-    """bench.py's lib_comm_init: the ranks agree over the gloo control group
-    whether the library's communicator is usable; if any rank's init failed,
-    every rank falls back (and a rank whose init succeeded destroys it), so no
-    rank waits in an RCCL collective the others never enter."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, fail, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = dict((r, (ok, j, d)) for (r, ok, j, d) in (q.get(timeout=120) for _ in range(2)))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    want_ok = not fail
-    for r in range(2):
-        (ok, joined, destroyed) = got[r]
-        assert ok == want_ok
-        assert destroyed == (joined and not want_ok)
