@@ -1340,4 +1340,15 @@ if __name__ == "__main__":
     _rc = maybe_relaunch(_args, sys.argv[1:])
     if _rc is not None:
         sys.exit(_rc)
-    sys.exit(main() or 0)
+    try:
+        _rc = main() or 0
+    except SystemExit as _e:
+        if _e.code != 3:
+            raise
+        # a rank could not join the communicator (lib_comm_init): leave at once,
+        # without the interpreter's teardown (an abandoned RCCL init may still
+        # sit in its bootstrap on a library thread)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3)
+    sys.exit(_rc)

@@ -11,12 +11,15 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -31,6 +34,14 @@ namespace {
 static bool trace_alloc() {
     static const bool on = [] {
         const char* e = getenv("MASTIC_TRACE_ALLOC");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+// MASTIC_TRACE_COMM=1: log the communicator's init / agreement / abort steps (stderr)
+static bool trace_comm() {
+    static const bool on = [] {
+        const char* e = getenv("MASTIC_TRACE_COMM");
         return e && e[0] == '1';
     }();
     return on;
@@ -1111,6 +1122,15 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         } else if (l > 0 && !hit) {
             if (launch_absorb(l - 1, aes_done, e4, e5, ss)) return -1;
         } else {
+            if (c->sponge_delay_us > 0) {
+                // test hook: the sponge stream is still busy when these (empty)
+                // marks are recorded there; nothing on the main stream waits for them
+                const unsigned long long ticks =
+                    (unsigned long long)c->sponge_delay_us * (unsigned long long)c->wall_khz / 1000;
+                c->sponge_delay_us = 0;
+                hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, ss, ticks);
+                HIPCHK(c, hipGetLastError());
+            }
             HIPCHK(c, hipEventRecord(e4, ss));
             HIPCHK(c, hipEventRecord(e5, ss));
         }
@@ -1234,13 +1254,6 @@ extern "C" int mastic_prep_init(mastic_ctx* c, mastic_reports* rep, const uint8_
     static const uint8_t empty_vk[1] = {0};
     if (!verify_key) verify_key = empty_vk;
     c->tcur = agg_id;
-    if (c->sponge_delay_us > 0) {
-        // test hook: the sponge stream is busy when this call records its marks there
-        const unsigned long long ticks = (unsigned long long)c->sponge_delay_us * (unsigned long long)c->wall_khz / 1000;
-        c->sponge_delay_us = 0;
-        hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, c->stream2, ticks);
-        HIPCHK(c, hipGetLastError());
-    }
     Tree* t = nullptr;
     int rc = build_tree(c, enc_agg_param, agg_param_len, &t);
     if (rc) return rc;
@@ -1721,10 +1734,11 @@ extern "C" int mastic_fold_shares(mastic_ctx* c, const void* dev_shares, size_t 
 // every rank is ready do the data all-gather and the GF(p) fold run.  Every
 // wait on the communicator is bounded by the ctx's timeout
 // (mastic_comm_init_timeout): a peer that never joins (it crashed, or is stuck
-// elsewhere) becomes MASTIC_ETIMEDOUT, and the communicator is aborted
-// (ncclCommAbort); later collective calls then fail with MASTIC_EHIP -- never
-// a silent world-1 merge -- until mastic_comm_destroy and a new
-// mastic_comm_init.
+// elsewhere) becomes MASTIC_ETIMEDOUT.  An init that times out is abandoned
+// (its thread keeps it; the ctx stays world 1); a collective that times out
+// aborts the communicator (ncclCommAbort), and later collective calls then
+// fail with MASTIC_EHIP -- never a silent world-1 merge -- until
+// mastic_comm_destroy and a new mastic_comm_init.
 
 namespace {
 // RCCL is bound on first use of a communicator entry point (dlopen), so a
@@ -1734,7 +1748,6 @@ struct RcclApi {
     bool ok = false;
     std::string why;
     decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
-    decltype(&ncclCommInitRankConfig) CommInitRankConfig = nullptr;
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
     decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
     decltype(&ncclCommAbort) CommAbort = nullptr;
@@ -1762,7 +1775,6 @@ const RcclApi& rccl() {
             all = all && fn;
         };
         bind(a.GetUniqueId, "ncclGetUniqueId");
-        bind(a.CommInitRankConfig, "ncclCommInitRankConfig");
         bind(a.CommInitRank, "ncclCommInitRank");
         bind(a.CommGetAsyncError, "ncclCommGetAsyncError");
         bind(a.CommAbort, "ncclCommAbort");
@@ -1788,6 +1800,16 @@ struct CommStatus {
 static_assert(sizeof(CommStatus) == 32, "CommStatus layout");
 constexpr uint32_t COMM_MAGIC = 0x4d415354u;
 enum CommOp : uint32_t { COMM_ALLGATHER_FOLD = 1, COMM_MERGE_HOST = 2, COMM_AGGREGATE_MERGED = 3 };
+
+// One communicator init on its own thread (mastic_comm_init_timeout).
+struct CommInitJob {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclSuccess;
+    hipError_t dev_err = hipSuccess;
+};
 const char* comm_op_name(uint32_t op) {
     return op == COMM_ALLGATHER_FOLD ? "mastic_allgather_fold"
            : op == COMM_MERGE_HOST   ? "mastic_merge_host"
@@ -1812,14 +1834,19 @@ static int comm_abort(mastic_ctx* c, int code, const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
-    if (c->comm) (void)rccl().CommAbort(c->comm);
+    if (trace_comm()) fprintf(stderr, "[mastic comm] abort: %s\n", buf);
+    if (c->comm) {
+        const ncclResult_t r = rccl().CommAbort(c->comm);
+        if (trace_comm()) fprintf(stderr, "[mastic comm] ncclCommAbort -> %d\n", (int)r);
+    }
     c->comm = nullptr;
     c->comm_broken = true;
     return fail(c, code, "%s; the communicator was aborted", buf);
 }
 
-// A non-blocking communicator's call may return ncclInProgress: poll its
-// state until it settles, within the ctx's timeout.
+// The result of an RCCL call on the ctx's communicator; a call that reports
+// ncclInProgress (a non-blocking communicator's) is polled until it settles,
+// within the ctx's timeout.
 static int comm_settle(mastic_ctx* c, ncclResult_t r, const char* what) {
     const double t0 = now_ms();
     while (r == ncclInProgress) {
@@ -2003,32 +2030,52 @@ extern "C" int mastic_comm_init_timeout(mastic_ctx* c, int nranks, int rank, con
     }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    // Non-blocking init, so a peer that never joins ends in a timeout and
-    // ncclCommAbort rather than a hang.  The config claims the 2.14 layout,
-    // whose fields every later RCCL reads (the process may hold an RCCL other
-    // than this header's, e.g. PyTorch's); an RCCL that refuses the config
-    // gets the blocking init.
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.version = NCCL_VERSION(2, 14, 0);
-    cfg.blocking = 0;
-    ncclComm_t comm = nullptr;
-    ncclResult_t r = rccl().CommInitRankConfig(&comm, nranks, uid, rank, &cfg);
-    if (r == ncclInvalidArgument && !comm) r = rccl().CommInitRank(&comm, nranks, uid, rank);
-    if (r != ncclSuccess && r != ncclInProgress) {
-        if (comm) (void)rccl().CommAbort(comm);
-        return fail(c, MASTIC_EHIP, "RCCL init: %s", rccl().GetErrorString(r));
+    // RCCL's init blocks until every rank has joined -- in its bootstrap,
+    // even for a communicator configured non-blocking (measured on RCCL
+    // 2.27.7: ncclCommInitRankConfig with blocking = 0 did not return while
+    // a peer was missing) -- so it runs on a thread of its own and this call
+    // waits for it with the ctx's bound.  An init the caller gave up on stays
+    // with its thread, which releases the communicator (ncclCommAbort) if the
+    // peers ever arrive; the ctx stays world 1.
+    auto job = std::make_shared<CommInitJob>();
+    const int dev = c->device;
+    try {
+        std::thread([job, nranks, uid, rank, dev] {
+            ncclComm_t comm = nullptr;
+            ncclResult_t r = ncclSystemError;
+            const hipError_t e = hipSetDevice(dev);
+            if (e == hipSuccess) r = rccl().CommInitRank(&comm, nranks, uid, rank);
+            std::unique_lock<std::mutex> lk(job->mu);
+            job->comm = comm;
+            job->r = r;
+            job->dev_err = e;
+            job->done = true;
+            const bool given_up = job->abandoned;
+            lk.unlock();
+            job->cv.notify_all();
+            if (given_up && comm) (void)rccl().CommAbort(comm);
+        }).detach();
+    } catch (const std::system_error&) {
+        return fail(c, MASTIC_EHIP, "cannot start the RCCL init thread");
     }
-    c->comm = comm;
+    std::unique_lock<std::mutex> lk(job->mu);
+    if (!job->cv.wait_for(lk, std::chrono::milliseconds(c->comm_timeout_ms), [&] { return job->done; })) {
+        job->abandoned = true;
+        if (trace_comm()) fprintf(stderr, "[mastic comm] init of rank %d of %d timed out\n", rank, nranks);
+        return fail(c, MASTIC_ETIMEDOUT,
+                    "RCCL init: not every rank joined within %d ms (the pending init is abandoned; the ctx stays "
+                    "world 1)", c->comm_timeout_ms);
+    }
+    if (trace_comm()) fprintf(stderr, "[mastic comm] ncclCommInitRank(%d of %d) -> %d\n", rank, nranks, (int)job->r);
+    if (job->dev_err != hipSuccess) return fail(c, MASTIC_EHIP, "hipSetDevice: %s", hipGetErrorString(job->dev_err));
+    if (job->r != ncclSuccess) {
+        if (job->comm) (void)rccl().CommAbort(job->comm);
+        return fail(c, MASTIC_EHIP, "RCCL init: %s", rccl().GetErrorString(job->r));
+    }
+    c->comm = job->comm;
     c->comm_n = nranks;
     c->comm_rank = rank;
     c->comm_broken = false;
-    int rc = comm_settle(c, r, "init");
-    if (rc) {
-        c->comm_n = 1;
-        c->comm_rank = 0;
-        c->comm_broken = false;  // nothing was joined: the ctx is world 1 again
-        return rc;
-    }
     return 0;
 }
 

@@ -405,8 +405,9 @@ class Mastic:
 
     def set_test_sponge_delay(self, delay_us: int):
         """Test hook (``mastic_set_test_sponge_delay``): the next prep_init
-        first holds the binder-sponge stream for ``delay_us`` microseconds,
-        so its timing marks there complete late.  Results are unaffected."""
+        that records empty timing marks on the binder-sponge stream (a
+        frontier-cache hit) first holds that stream for ``delay_us``
+        microseconds, so those marks complete late.  Results are unaffected."""
         _check(self._ctx, _lib.lib().mastic_set_test_sponge_delay(self._ctx, int(delay_us)))
 
     def set_frontier_cache(self, on: bool):

@@ -195,10 +195,12 @@ int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares,
  * error, every other rank the code of the lowest failing rank; calls that
  * disagree on the entry point, n_local or n_elems return MASTIC_EINVAL on
  * every rank.  Every wait on the communicator (init included) is bounded by
- * the ctx's timeout: a peer that never joins yields MASTIC_ETIMEDOUT, and the
- * communicator is then aborted -- later collective calls fail with
- * MASTIC_EHIP (never a silent world-1 merge) until mastic_comm_destroy and a
- * new mastic_comm_init. */
+ * the ctx's timeout: a peer that never joins yields MASTIC_ETIMEDOUT.  A
+ * timed-out init is abandoned (the ctx stays world 1; RCCL's pending init
+ * stays on a library thread, which releases the communicator if the peers
+ * ever arrive); a timed-out collective aborts the communicator, and later
+ * collective calls fail with MASTIC_EHIP (never a silent world-1 merge) until
+ * mastic_comm_destroy and a new mastic_comm_init. */
 #define MASTIC_COMM_ID_BYTES 128
 #define MASTIC_COMM_TIMEOUT_MS 120000 /* mastic_comm_init's bound on every communicator wait */
 int mastic_comm_unique_id(uint8_t id_out[MASTIC_COMM_ID_BYTES]);
@@ -280,10 +282,12 @@ int mastic_abi_version(void);
  * Outputs are identical either way.  Returns the number of injected failures
  * the previous setting still had pending (>= 0), or MASTIC_EINVAL. */
 int mastic_set_test_hooks(mastic_ctx* ctx, int force_slow_blk, int fail_allocs);
-/* Test hook: the next mastic_prep_init first queues a kernel that idles
- * delay_us microseconds (0..10^7) on the ctx's binder-sponge stream, so the
- * timing marks that call records there complete late (mastic_last_timing*
- * must wait for them).  Results are unaffected. */
+/* Test hook: the next mastic_prep_init that records empty timing marks on
+ * the ctx's binder-sponge stream (level 0 of a call, a frontier-cache hit)
+ * first queues there a kernel that idles delay_us microseconds (0..10^7), so
+ * those marks complete late while nothing on the main stream waits for them
+ * (mastic_last_timing* must wait for the marks themselves).  Results are
+ * unaffected. */
 int mastic_set_test_sponge_delay(mastic_ctx* ctx, int delay_us);
 
 /* One-shot host-buffer form of upload + prep_init + prep_result. */

@@ -11,6 +11,11 @@
 //                 the transposes' share
 //   tt_ctr        the T-table with counter groups (aes.hpp ctr_blocks_n, N = 2),
 //                 the level kernel's payload loop, same per-lane keys
+//   tt_ctr_ukey   the same T-table loop with ONE wave-uniform key schedule
+//                 (round 6): the 44 key words read once into
+//                 SGPRs (readfirstlane), so a round's key costs no LDS read --
+//                 what one report's convert stream spread over a wave's lanes
+//                 (consecutive counter blocks per lane) would allow
 // Blocks per second over the chip and per CU-clock.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -o tools/aes_bs_mb tools/aes_bs_mb.hip
 // Not part of the product.
@@ -20,6 +25,7 @@
 MH_D uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 #include "aes_bs.hpp"
 #include <stdio.h>
+#include <stdlib.h>
 
 struct BmBfe {  // broadcast mask of a lane's data bit
     MH_D uint32_t operator()(uint32_t v, int bit) const { return (uint32_t)__builtin_amdgcn_sbfe((int)v, bit, 1); }
@@ -42,10 +48,10 @@ struct KmUniform {  // wave-uniform key words (SGPRs)
     }
 };
 
-// MODE 0 bs, 1 bs_ukey, 2 bs_notr, 3 tt_ctr
+// MODE 0 bs, 1 bs_ukey, 2 bs_notr, 3 tt_ctr, 4 tt_ctr_ukey
 template <int MODE, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_mb(uint32_t* out, const uint32_t* ukey, int iters) {
-    constexpr bool TT = MODE == 3;
+    constexpr bool TT = MODE == 3 || MODE == 4;
     extern __shared__ uint32_t lds[];
     uint32_t* T = lds;  // T-table (AesPerm layout, must sit at LDS address 0) for MODE 3
     uint4* RK = (uint4*)(lds + (TT ? AES_PERM_LDS_WORDS : 0));
@@ -65,7 +71,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_mb(uint32_t* out, const uint32_t
         asm volatile("" ::: "memory");
         if constexpr (TT) {
             const AesPerm TL{T, 4u * (uint32_t)(lane & 31), 128u + 4u * (uint32_t)(lane & 31)};
-            const RkLds rk{row};
+            uint32_t kw[44];
+            if constexpr (MODE == 4) {
+#pragma unroll
+                for (int i = 0; i < 44; i++) kw[i] = __builtin_amdgcn_readfirstlane(ukey[i]);
+            }
+            const RkLds rkl{row};
+            const RkRegs rkr{kw};
+            const auto& rk = [&]() -> const auto& {
+                if constexpr (MODE == 4) return rkr; else return rkl;
+            }();
             // 32 blocks of one seed as the payload loop does them: one counter
             // group per 256 counters, pairs in lockstep
             AesCtrGroup g;
@@ -120,7 +135,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_mb(uint32_t* out, const uint32_t
 
 template <int MODE, int WAVES>
 void run(uint32_t* out, const uint32_t* ukey, int grid, const char* name) {
-    const size_t lds = (MODE == 3 ? AES_PERM_LDS_WORDS * 4 : 0) + 64 * 11 * 16;
+    const size_t lds = (MODE == 3 || MODE == 4 ? AES_PERM_LDS_WORDS * 4 : 0) + 64 * 11 * 16;
     hipFuncSetAttribute((const void*)k_mb<MODE, WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncAttributes fa;
     hipFuncGetAttributes(&fa, (const void*)k_mb<MODE, WAVES>);
@@ -154,6 +169,8 @@ int main() {
     hipMemset(ukey, 0x5a, 64 * sizeof(uint32_t));
     for (int rep = 0; rep < 2; rep++) {
         run<3, 16>(out, ukey, 256 * 4, "tt_ctr (T-table, counter groups, pairs) w16");
+        run<4, 16>(out, ukey, 256 * 4, "tt_ctr_ukey (same, one wave-uniform key in SGPRs) w16");
+        if (getenv("AES_MB_TT_ONLY")) continue;
         run<0, 4>(out, ukey, 256 * 16, "bs w4");
         run<0, 8>(out, ukey, 256 * 8, "bs w8");
         run<1, 4>(out, ukey, 256 * 16, "bs_ukey w4");
