@@ -111,6 +111,10 @@ def parse():
     ap.add_argument("--lib", default="",
                     help="A/B tools only: bind this build of libmastic_hip (e.g. an experiment-knobs build) "
                          "instead of the shipped one; the JSON line then names it under 'library'")
+    ap.add_argument("--standalone", type=int, default=1,
+                    help="after the timed region, one more step (c2) / sweep (sweep configs) with every binder-sponge "
+                         "launch running alone (Mastic.set_serial_sponges): the sponge kernels' and the level "
+                         "kernel's own rooflines; 0 skips it")
     ap.add_argument("--north-star-reports", type=int, default=0,
                     help="job size of the north_star leg (0 = the 1M of BASELINE.json; smaller only for rehearsals)")
     return ap.parse_args()
@@ -576,6 +580,18 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
     (free_b, total_b) = torch.cuda.mem_get_info()
     hbm_used = (total_b - free_b) / 1e9  # whole device, arena and frontier cache included
     dt = max_over_ranks(dist, torch, dt)
+    # the same sweep once more with every binder-sponge launch running alone
+    # (results identical; its trajectory is the timed sweep's): the sponge
+    # kernels' and the level kernel's own rates, beside the co-running ones
+    timing_alone = None
+    if getattr(args, "standalone", 1):
+        m.set_serial_sponges(True)
+        timing_alone = []
+        step(None, timing_alone)
+        m.set_serial_sponges(False)
+        m.synchronize()
+        if dist:
+            dist.barrier()
 
     # units: reports x candidates of both aggregators at every level, over the job
     # (the ranks' shares sum to the job; a virtual rank reports its own share)
@@ -721,7 +737,7 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             "frac": (ab_perms * KECCAK_OPS / (sum(per_level["absorb_ms"]) / 1e3) / 1e12 / VALU_PEAK_TOPS)
             if sum(per_level["absorb_ms"]) > 0 else 0.0,
             "note": "Keccak-p of the one-hot and payload binders over the summed duration of the sponge launches "
-                    "(which run beside the level kernels)",
+                    "(which run beside the level kernels in the timed sweep; `standalone`: alone)",
         },
         "breakdown_ms_per_step": {
             # every algorithmic op of the AES and Keccak kernels (level kernels: nodes x ops per
@@ -736,6 +752,21 @@ def run_sweep(args, cfg, world, rank, local, dist, torch, split=None, steps=None
             "host_phases_ms": {k: v * 1e3 / steps for (k, v) in phases.items()},
         },
     }
+    if timing_alone:
+        ab_alone_ms = sum(x[4] for x in timing_alone)
+        lk_alone_ms = sum(x[0] + x[2] for x in timing_alone)
+        nodes_one = nodes // steps
+        out["roofline_absorb"]["standalone"] = {
+            "frac": ab_perms * KECCAK_OPS / (ab_alone_ms / 1e3) / 1e12 / VALU_PEAK_TOPS if ab_alone_ms > 0 else None,
+            "sponge_ms": ab_alone_ms,
+            "level_kernel_frac_alone": nodes_one * dom_ops / (lk_alone_ms / 1e3) / 1e12 / VALU_PEAK_TOPS
+            if lk_alone_ms > 0 else None,
+            "level_kernel_ms_alone": lk_alone_ms,
+            "what": "one more sweep (same trajectory) with every binder-sponge launch running alone "
+                    "(Mastic.set_serial_sponges: the level kernels wait for it); frac = the same Keccak-p over the "
+                    "summed sponge-launch durations; level_kernel_frac_alone = the level kernel without sponges "
+                    "beside it",
+        }
     out["rates"] = {
         "with_frontier_cache" if args.frontier_cache else "spec_literal": units / dt,
         "unit": "report*prefix/s (both aggregators' prep_init + decide + fold per level, whole sweep)",
@@ -1063,6 +1094,17 @@ def main():
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dist, torch, dt)
 
+    alone = None
+    if getattr(args, "standalone", 1):
+        # one more step with every binder-sponge launch running alone (results
+        # identical): the sponge kernel's and the level kernel's own rates
+        m.set_serial_sponges(True)
+        step(slices[0])
+        alone = m.last_timing3()
+        m.set_serial_sponges(False)
+        m.synchronize()
+        if dist:
+            dist.barrier()
     units = n_rep * len(attrs) * args.steps * world
     value = units / dt
     # roofline of the dominant kernel: algorithmic int32 ops (fixed convention).
@@ -1133,14 +1175,30 @@ def main():
     # beside the level kernel for most of the step)
     ab_perms = absorb_perms * n_rep * args.steps
     ab_ach = ab_perms * KECCAK_OPS / (absorb_ms / 1e3) / 1e12 if absorb_ms > 0 else 0.0
+    standalone = None
+    if alone is not None:
+        (a_ea, _a_na, a_ep, _a_np, a_eb, _a_nb, _a_t) = alone
+        standalone = {
+            "frac": absorb_perms * n_rep * KECCAK_OPS / (a_eb / 1e3) / 1e12 / VALU_PEAK_TOPS if a_eb > 0 else None,
+            "sponge_ms": a_eb,
+            "level_kernel_frac_alone": nodes * n_rep * (aes_ops_node + KECCAK_OPS) / ((a_ea + a_ep) / 1e3) / 1e12
+            / VALU_PEAK_TOPS if a_ea + a_ep > 0 else None,
+            "level_kernel_ms_alone": a_ea + a_ep,
+            "what": "one more step with every binder-sponge launch running alone (Mastic.set_serial_sponges: the "
+                    "level kernels wait for it); frac = the step's Keccak-p over the summed sponge-launch "
+                    "durations; at this batch the sponges are one dependent chain per report (%d waves for the "
+                    "chip's 1,024 SIMDs), i.e. latency-bound, and hidden under the level kernel in the timed "
+                    "steps" % ((n_rep * 2 * 2 + 63) // 64),
+        }
     out["roofline_absorb"] = {
+        "standalone": standalone,
         "kernel": "k_absorb_pair (2 lanes per sponge)" if n_rep < 65536 else "k_absorb (1 lane per sponge)",
         "keccak_perms_per_report": absorb_perms,
         "achieved": ab_ach, "peak": VALU_PEAK_TOPS, "unit": "Tops/s (int32)", "frac": ab_ach / VALU_PEAK_TOPS,
         "ms_per_step": absorb_ms / args.steps,
         "note": "one-hot 32 B per node + payload VL*ENC B per interior node, / 168 B per Keccak-p[1600,12] "
-                "(3,720 ops); the sponges run beside the level kernel, so this is their share of the step's "
-                "VALU, not a standalone rate",
+                "(3,720 ops); the timed steps run the sponges beside the level kernel, so `frac` is their share "
+                "of the step's VALU; `standalone` times them alone",
     }
     # HBM bytes per launch of the dominant kernel from the PMC passes (profiles/eval_traffic.json),
     # when they were measured at this exact workload

@@ -240,7 +240,7 @@ struct mastic_ctx {
     int sponge_delay_us = 0;    // the next prep_init first holds the sponge stream this long (k_spin)
     int wall_khz = 100000;      // wall_clock64() rate (hipDeviceAttributeWallClockRate)
     bool timing_nowait = false; // A/B of the last_timing fix only (MASTIC_DBG_TIMING_NOWAIT, knob builds)
-    bool serial_sponges = false;  // timing only: sponge launches run alone (MASTIC_SERIAL_SPONGES, knob builds)
+    bool serial_sponges = false;  // measurement: sponge launches run alone (mastic_set_serial_sponges)
     bool inject_alloc_failure() {
         if (fail_allocs <= 0) return false;
         fail_allocs--;
@@ -939,7 +939,7 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
         HIPCHK(c, hipGetLastError());
         *done = get_sync_event(c, sev++);
         HIPCHK(c, hipEventRecord(*done, as));
-        // timing experiments only (MASTIC_SERIAL_SPONGES): the main stream waits
+        // measurement schedule (mastic_set_serial_sponges): the main stream waits
         // for this launch, so it runs alone on the chip (standalone sponge rate)
         if (c->serial_sponges && as != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, *done, 0));
         if (which0 == 0) f_oh = (f_oh + ab.nbytes[0]) % KECCAK_RATE;
@@ -2730,6 +2730,13 @@ extern "C" int mastic_set_test_hooks(mastic_ctx* c, int force_slow_blk, int fail
     c->force_slow_blk = force_slow_blk < 0 ? -1 : force_slow_blk;
     c->fail_allocs = std::max(0, fail_allocs);
     return pending;
+}
+
+extern "C" int mastic_set_serial_sponges(mastic_ctx* c, int on) {
+    if (!c) return MASTIC_EINVAL;
+    const int prev = c->serial_sponges ? 1 : 0;
+    if (on >= 0) c->serial_sponges = on != 0;
+    return prev;
 }
 
 extern "C" int mastic_set_test_sponge_delay(mastic_ctx* c, int delay_us) {

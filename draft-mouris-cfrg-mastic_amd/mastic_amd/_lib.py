@@ -34,7 +34,7 @@ EXPORTS = [
     "mastic_work_bytes", "mastic_last_timing3", "mastic_proof_tree", "mastic_set_frontier_cache",
     "mastic_reports_view", "mastic_decide_results",
     "mastic_aggregate_device_on_stream", "mastic_abi_version", "mastic_set_test_hooks",
-    "mastic_set_test_sponge_delay",
+    "mastic_set_test_sponge_delay", "mastic_set_serial_sponges",
     "mastic_comm_unique_id", "mastic_comm_init", "mastic_comm_init_timeout", "mastic_comm_info",
     "mastic_comm_destroy",
     "mastic_allgather_fold", "mastic_aggregate_merged", "mastic_merge_host",
@@ -158,6 +158,7 @@ def lib():
                     "mastic_abi_version": (i32, []),
                     "mastic_set_test_hooks": (i32, [P, i32, i32]),
                     "mastic_set_test_sponge_delay": (i32, [P, i32]),
+                    "mastic_set_serial_sponges": (i32, [P, i32]),
                     "mastic_reports_view": (i32, [P, sz, sz, ctypes.POINTER(P)]),
                     "mastic_decide_results": (i32, [P, u8p, sz, P, P]),
                     "mastic_last_timing3": (i32, [P] + [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)] * 3

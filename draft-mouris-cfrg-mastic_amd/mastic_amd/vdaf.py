@@ -410,6 +410,18 @@ class Mastic:
         microseconds, so those marks complete late.  Results are unaffected."""
         _check(self._ctx, _lib.lib().mastic_set_test_sponge_delay(self._ctx, int(delay_us)))
 
+    def set_serial_sponges(self, on=None) -> bool:
+        """Measurement schedule (``mastic_set_serial_sponges``): with ``on``
+        True every binder-sponge launch runs alone on the GPU (the level
+        kernels wait for it), so ``last_timing3`` times the sponge kernels and
+        the level kernel each by itself; False restores the overlapped
+        schedule, None only queries.  Results are identical either way.
+        Returns the previous setting."""
+        rc = _lib.lib().mastic_set_serial_sponges(self._ctx, -1 if on is None else int(bool(on)))
+        if rc < 0:
+            _check(self._ctx, rc)
+        return bool(rc)
+
     def set_frontier_cache(self, on: bool):
         """Keep each prep_init's per-level binder inputs and last frontier in HBM so
         that the next level of a sweep evaluates only its new level (C ABI

@@ -264,6 +264,13 @@ int mastic_proof_tree(mastic_ctx* ctx, int agg_id, const uint8_t* app_ctx, size_
  * are identical either way.  *last_hit (if not NULL) = 1 when the last
  * prep_init took the cached path. */
 int mastic_set_frontier_cache(mastic_ctx* ctx, int on, int* last_hit);
+/* Measurement schedule: on = 1 makes every binder-sponge launch run alone
+ * (the level kernels wait for it instead of running beside it), so the
+ * sponge kernels' and the level kernel's own rates can be timed
+ * (mastic_last_timing3); 0 restores the overlapped schedule, -1 only queries.
+ * Results are identical either way.  Returns the previous setting (0 / 1) or
+ * MASTIC_EINVAL. */
+int mastic_set_serial_sponges(mastic_ctx* ctx, int on);
 /* Wait for all enqueued work of the ctx. */
 int mastic_synchronize(mastic_ctx* ctx);
 /* The library's MASTIC_ABI_VERSION (a caller built against another header
