@@ -2,6 +2,13 @@ import os
 import sys
 
 import pytest
+# torch first: libmastic_hip.so then binds the HIP runtime torch already loaded
+# (same soname), as in bench.py.  A test module that creates a Mastic ctx
+# before anything imports torch would otherwise load /opt/rocm's runtime
+# first, and torch's own copy, loaded second, then sees no GPU
+# (torch.cuda.is_available() False: gpurun_out r06_v6, tests/test_gpu_comm.py
+# after tests/test_gpu_serial_sponges.py).
+import torch  # noqa: F401,E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_ROOT = os.path.join(ROOT, "draft-mouris-cfrg-mastic_amd")
