@@ -24,6 +24,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "comm_agree.hpp"
 #include "host_tree.hpp"
 #include "kernels.hpp"
 #include "shard.hpp"
@@ -1788,19 +1789,6 @@ const RcclApi& rccl() {
     return api;
 }
 
-// One rank's record in the agreement round of a collective call.
-struct CommStatus {
-    int32_t rc;        // 0 = this rank's local work succeeded, else its MASTIC_E* code
-    uint32_t op;       // entry point (CommOp)
-    uint64_t n_local;  // shares per rank
-    uint64_t n_elems;  // elements per share
-    uint32_t magic;
-    uint32_t pad;
-};
-static_assert(sizeof(CommStatus) == 32, "CommStatus layout");
-constexpr uint32_t COMM_MAGIC = 0x4d415354u;
-enum CommOp : uint32_t { COMM_ALLGATHER_FOLD = 1, COMM_MERGE_HOST = 2, COMM_AGGREGATE_MERGED = 3 };
-
 // One communicator init on its own thread (mastic_comm_init_timeout).
 struct CommInitJob {
     std::mutex mu;
@@ -1925,23 +1913,17 @@ static int comm_agree(mastic_ctx* c, int local_rc, uint32_t op, size_t n_local, 
     }
     rc = comm_wait(c, "status all-gather");
     if (rc) return local_rc ? local_rc : rc;
-    int first_bad = -1, mismatch = -1;
-    for (int r = 0; r < c->comm_n; r++) {
-        const CommStatus& s = h[1 + r];
-        if (s.magic != COMM_MAGIC || s.op != op || s.n_local != n_local || s.n_elems != n_elems) {
-            if (mismatch < 0) mismatch = r;
-        } else if (s.rc != 0 && first_bad < 0) {
-            first_bad = r;
-        }
-    }
+    const CommVerdict v = comm_decide(h + 1, c->comm_n, op, n_local, n_elems);
+    const int rc_all = comm_rank_result(v, local_rc, MASTIC_EINVAL);
     if (local_rc) {
         c->err = local_err;
         return local_rc;
     }
-    if (first_bad >= 0)
-        return fail(c, h[1 + first_bad].rc, "%s failed on rank %d (code %d); no shares were exchanged",
-                    comm_op_name(op), first_bad, h[1 + first_bad].rc);
-    if (mismatch >= 0) {
+    if (v.first_bad >= 0)
+        return fail(c, rc_all, "%s failed on rank %d (code %d); no shares were exchanged", comm_op_name(op),
+                    v.first_bad, v.bad_rc);
+    if (v.mismatch >= 0) {
+        const int mismatch = v.mismatch;
         const CommStatus& s = h[1 + mismatch];
         return fail(c, MASTIC_EINVAL,
                     "ranks disagree on the collective call: rank %d called %s with %llu x %llu elements, this rank "
