@@ -1798,11 +1798,6 @@ struct CommInitJob {
     ncclResult_t r = ncclSuccess;
     hipError_t dev_err = hipSuccess;
 };
-const char* comm_op_name(uint32_t op) {
-    return op == COMM_ALLGATHER_FOLD ? "mastic_allgather_fold"
-           : op == COMM_MERGE_HOST   ? "mastic_merge_host"
-           : op == COMM_AGGREGATE_MERGED ? "mastic_aggregate_merged" : "?";
-}
 }  // namespace
 
 // ctx teardown: its queued work is waited for, then the communicator is
