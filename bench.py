@@ -291,6 +291,9 @@ def lib_comm_init(m, dist, world, rank, timeout_ms=0):
     ok = 1
     if err is None and not uid:
         err = RuntimeError("rank 0 could not create the communicator id")
+    if err is None and os.environ.get("MASTIC_BENCH_COMM_FAIL_RANK") == str(rank):
+        # tests/test_gpu_bench_2rank.py: a rank whose init fails (the exit path end to end)
+        err = RuntimeError("injected by MASTIC_BENCH_COMM_FAIL_RANK")
     if err is None:
         try:
             m.comm_init(world, rank, uid, timeout_ms)

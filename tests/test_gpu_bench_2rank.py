@@ -32,6 +32,9 @@ def test_bench_two_ranks_on_one_gpu():
     assert "error" not in ns, ns
     assert ns["n_gpus"] == 2 and ns["scaling"] == "strong" and ns["job_reports"] == 16384
     assert ns["heavy_hitters_equal_plaintext"] is True
+    for c in (d["comm"], ns["comm"]):  # the merge path the line was measured with
+        assert c["backend"] == "gloo-rehearsal" and c["nranks"] == 2
+        assert [x["rank"] for x in c["devices"]] == [0, 1]
 
 
 def _run_bench(args, timeout=500):
@@ -109,3 +112,31 @@ def test_bench_under_torchrun_uses_the_library_communicator():
     ns = d["north_star"]
     assert "error" not in ns, ns
     assert ns["job_reports"] == 16384 and ns["heavy_hitters_equal_plaintext"] is True
+    for c in (d["comm"], ns["comm"]):
+        assert c["backend"] == "rccl" and c["nranks"] == 1 and len(c["devices"]) == 1
+    # the sponge kernels' and the level kernel's own rates (Mastic.set_serial_sponges)
+    for ab in (d["roofline_absorb"], ns["roofline_absorb"]):
+        assert ab["standalone"]["frac"] > 0 and ab["standalone"]["level_kernel_frac_alone"] > 0
+
+
+def test_bench_exits_nonzero_when_a_rank_cannot_join():
+    """No silent fallback: under torch.distributed.run with the nccl backend, a
+    rank whose library communicator cannot be created (injected) makes the
+    run exit non-zero with no bench line, instead of switching to another
+    merge transport."""
+    import socket
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "1",
+           "--warmup", "0", "--reports", "512", "--total-reports", "512", "--north-star", "0", "--cpu-baseline", "0"]
+    env = dict(os.environ, MASTIC_BENCH_COMM_FAIL_RANK="0")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "no silent fallback" in r.stderr
