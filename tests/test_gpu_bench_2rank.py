@@ -79,8 +79,10 @@ def test_bench_four_ranks_one_rank_without_reports():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    # (--standalone 0: this case is about the empty rank; four ranks sharing one GPU take ~100 s
+    # per sweep of 32 merged levels already)
     d = _run_bench(["--gpus", "4", "--config", "c2sweep", "--split", "1", "--reports", "3", "--steps", "1",
-                    "--warmup", "0", "--cpu-baseline", "0", "--memory-budget-gb", "2"])
+                    "--warmup", "0", "--cpu-baseline", "0", "--memory-budget-gb", "2", "--standalone", "0"])
     c = d["config"]
     assert d["n_gpus"] == 4 and c["job_reports"] == 3 and c["reports_this_rank"] == 0
     assert c["heavy_hitters_equal_plaintext"] is True
