@@ -935,7 +935,8 @@ static int run_chunk(mastic_ctx* c, mastic_reports* rep, const Tree* t, const Wo
                                dim3((groups * 64 * 2 + c->absorb_threads - 1) / c->absorb_threads, (unsigned)nwh),
                                dim3(c->absorb_threads), c->absorb_lds, as, pl, ab);
         else
-            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, (unsigned)nwh), dim3(256), 0, as, pl, ab);
+            hipLaunchKernelGGL(k_absorb, dim3((groups * 64 + 255) / 256, (unsigned)nwh), dim3(256), c->absorb_lds, as,
+                               pl, ab);
         if (e5) HIPCHK(c, hipEventRecord(e5, as));
         HIPCHK(c, hipGetLastError());
         *done = get_sync_event(c, sev++);
@@ -2643,6 +2644,8 @@ extern "C" int mastic_ctx_create(const mastic_params* up, mastic_ctx** out) {
         hipFuncSetAttribute((const void*)k_eval_aes<F128, false, false, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, EVAL_LDS_BYTES) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_absorb_pair, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)k_absorb, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess) {
         delete c;
         return MASTIC_EHIP;
