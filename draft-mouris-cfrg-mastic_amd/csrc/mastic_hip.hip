@@ -1887,6 +1887,15 @@ static int comm_agree(mastic_ctx* c, int local_rc, uint32_t op, size_t n_local, 
                                         "(mastic_comm_destroy, then mastic_comm_init)");
         return local_rc;  // world 1
     }
+    // this rank's queued work (its prep_init, the local fold) first, unbounded:
+    // the timeout below then measures only the wait for the peers
+    {
+        const hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess && !local_rc) {
+            (void)hipGetLastError();
+            local_rc = fail(c, MASTIC_EHIP, "%s: local work failed: %s", comm_op_name(op), hipGetErrorString(e));
+        }
+    }
     const std::string local_err = c->err;
     CommStatus* h = (CommStatus*)c->comm_st_host;  // [0]: this rank's record, [1 + r]: rank r's
     h[0] = CommStatus{local_rc, op, (uint64_t)n_local, (uint64_t)n_elems, COMM_MAGIC, 0};

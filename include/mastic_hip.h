@@ -195,7 +195,9 @@ int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares,
  * error, every other rank the code of the lowest failing rank; calls that
  * disagree on the entry point, n_local or n_elems return MASTIC_EINVAL on
  * every rank.  Every wait on the communicator (init included) is bounded by
- * the ctx's timeout: a peer that never joins yields MASTIC_ETIMEDOUT.  A
+ * the ctx's timeout, which starts once this rank's own queued work is done
+ * (so a long prep_init ahead of a merge does not count against it): a peer
+ * that never joins yields MASTIC_ETIMEDOUT.  A
  * timed-out init is abandoned (the ctx stays world 1; RCCL's pending init
  * stays on a library thread, which releases the communicator if the peers
  * ever arrive); a timed-out collective aborts the communicator, and later
