@@ -40,9 +40,36 @@ MH_HD uint32_t aes_t0(int x) {
     return s2 | (s << 8) | (s << 16) | (s3 << 24);
 }
 
+// T0 words of all 256 S-box entries, built at compile time.  The table
+// fills below write runs of 64 words whose entries are wave-uniform, so each
+// run costs one scalar load of this table instead of a per-lane S-box byte
+// load whose latency the fill loop waited out 32 times per thread (~10 us per
+// level-kernel workgroup; profiles/r06_v12_*).
+struct AesT0Words {
+    uint32_t w[256];
+};
+constexpr AesT0Words aes_t0_words() {
+    AesT0Words t{};
+    for (int x = 0; x < 256; x++) {
+        const uint32_t s = AES_SBOX[x];
+        const uint32_t s2 = ((s << 1) ^ ((s & 0x80) ? 0x1bu : 0u)) & 0xffu;
+        t.w[x] = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
+    }
+    return t;
+}
+static constexpr AesT0Words AES_T0W = aes_t0_words();
+
 // Cooperative fill of the replicated table: T[(x << 5) | r] = T0[x].
+// nthreads: whole waves (tid = threadIdx.x).
 MH_D void aes_lds_fill(uint32_t* T, int tid, int nthreads) {
-    for (int i = tid; i < AES_LDS_WORDS; i += nthreads) T[i] = aes_t0(i >> 5);
+    const uint32_t lane = (uint32_t)tid & 63u;
+    const int w0 = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nthreads >> 6;
+#pragma unroll 8
+    for (int run = w0; run < AES_LDS_WORDS / 64; run += nw) {
+        // words [64 run, 64 run + 64): entries 2 run (lanes 0-31) and 2 run + 1
+        const uint32_t a = AES_T0W.w[2 * run], b = AES_T0W.w[2 * run + 1];
+        T[run * 64 + lane] = (lane & 32u) ? b : a;
+    }
 }
 
 struct AesLds {
@@ -221,11 +248,17 @@ MH_D void fixed_key_block2(const TT& T, const RK& rk, const uint32_t sa[4], uint
 #endif
 #define AES_PERM_LDS_WORDS (AES_T4 ? 256 * 128 : 256 * 64)
 
+// nthreads: whole waves (tid = threadIdx.x).  Word i = 64 run + lane holds
+// entry run & 255 (wave-uniform: one scalar load per run, AES_T0W) as T0 or
+// T2 (lanes 0-31 / 32-63), or T1 / T3 in the second block (run >= 256).
 MH_D void aes_perm_fill(uint32_t* T, int tid, int nthreads) {
-    for (int i = tid; i < AES_PERM_LDS_WORDS; i += nthreads) {
-        const uint32_t t0 = aes_t0((i >> 6) & 255);
-        const bool hi = i >= 256 * 64;  // T1 / T3 block
-        T[i] = (i & 32) ? (hi ? rot24(t0) : rot16(t0)) : (hi ? rot8(t0) : t0);
+    const uint32_t lane = (uint32_t)tid & 63u;
+    const int w0 = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nthreads >> 6;
+#pragma unroll 8
+    for (int run = w0; run < AES_PERM_LDS_WORDS / 64; run += nw) {
+        const uint32_t t0 = AES_T0W.w[run & 255];
+        const bool hi = run >= 256;  // T1 / T3 block
+        T[run * 64 + lane] = (lane & 32u) ? (hi ? rot24(t0) : rot16(t0)) : (hi ? rot8(t0) : t0);
     }
 }
 

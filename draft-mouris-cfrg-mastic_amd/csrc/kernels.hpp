@@ -786,11 +786,27 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     const int r = blockIdx.x * 64 + lane;
     const uint32_t lb = (uint32_t)r * 4u;
     {
+        // the two key schedules' 44 words per report: every wave's loads issued
+        // before any is waited for (one HBM round trip per workgroup, not three)
         uint32_t* ke = (uint32_t*)RKE;
         uint32_t* kc = (uint32_t*)RKC;
-        for (int i = wave; i < 44; i += EVAL_WAVES) {
-            ke[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_ext + (size_t)i * S, lb));
-            kc[lane * 44 + i] = aes_perm_key_word(i, pld(pl.rk_conv + (size_t)i * S, lb));
+        constexpr int KR = (44 + EVAL_WAVES - 1) / EVAL_WAVES;
+        uint32_t xe[KR], xc[KR];
+#pragma unroll
+        for (int j = 0; j < KR; j++) {
+            const int i = wave + j * EVAL_WAVES;
+            if (i < 44) {
+                xe[j] = pld(pl.rk_ext + (size_t)i * S, lb);
+                xc[j] = pld(pl.rk_conv + (size_t)i * S, lb);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < KR; j++) {
+            const int i = wave + j * EVAL_WAVES;
+            if (i < 44) {
+                ke[lane * 44 + i] = aes_perm_key_word(i, xe[j]);
+                kc[lane * 44 + i] = aes_perm_key_word(i, xc[j]);
+            }
         }
     }
     // words [8, 40): the fused-proof bitmap (FC) or, with split parents, each
