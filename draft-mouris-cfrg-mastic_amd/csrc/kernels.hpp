@@ -777,7 +777,6 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     // the T-table lookups use the v_perm result as the absolute LDS address
     // (aes.hpp lds_read_asm): the table must start at LDS address 0
     if ((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)eval_lds != 0u) __builtin_trap();
-    aes_perm_fill(T, threadIdx.x, 64 * EVAL_WAVES);
 
     const int S = pl.stride;
     const int S_in = FC ? a.in_stride : S;  // cs_in / fr_w_in
@@ -787,7 +786,8 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
     const uint32_t lb = (uint32_t)r * 4u;
     {
         // the two key schedules' 44 words per report: every wave's loads issued
-        // before any is waited for (one HBM round trip per workgroup, not three)
+        // first (one HBM round trip per workgroup, not three), the table filled
+        // while they are in flight, then the words stored
         uint32_t* ke = (uint32_t*)RKE;
         uint32_t* kc = (uint32_t*)RKC;
         constexpr int KR = (44 + EVAL_WAVES - 1) / EVAL_WAVES;
@@ -800,6 +800,7 @@ void k_eval_aes(McParams p, Planes pl, AesArgs a) {
                 xc[j] = pld(pl.rk_conv + (size_t)i * S, lb);
             }
         }
+        aes_perm_fill(T, threadIdx.x, 64 * EVAL_WAVES);
 #pragma unroll
         for (int j = 0; j < KR; j++) {
             const int i = wave + j * EVAL_WAVES;
