@@ -54,7 +54,9 @@ extern "C" {
  *    mastic_aggregate_device is removed -- its argument count changed
  *    between ABI 3, 4 and 5 -- and the stream form is
  *    mastic_aggregate_device_on_stream only, so a binary built against an
- *    older header fails to link instead of passing a garbage stream. */
+ *    older header fails to link instead of passing a garbage stream;
+ *    mastic_set_serial_sponges (measurement schedule), mastic_set_test_sponge_delay
+ *    (test hook). */
 #define MASTIC_ABI_VERSION 6
 
 #define MASTIC_OK 0
