@@ -187,6 +187,7 @@ struct mastic_ctx {
     hipStream_t stream4 = nullptr;  // FLP randomness + query of a weight-check call, beside its last sponges
     std::vector<hipEvent_t> sync_ev;
     hipEvent_t fold_ev = nullptr;  // mastic_fold_shares: producer stream -> stream
+    hipEvent_t comm_marks[3] = {};  // MASTIC_TRACE_COMM: progress marks of the agreement round
     // library-owned RCCL communicator (mastic_comm_init; none = world 1)
     ncclComm_t comm = nullptr;
     int comm_n = 1, comm_rank = 0;
@@ -315,6 +316,8 @@ struct mastic_ctx {
             for (auto e : x.ev) (void)hipEventDestroy(e);
         for (auto e : sync_ev) (void)hipEventDestroy(e);
         if (fold_ev) (void)hipEventDestroy(fold_ev);
+        for (hipEvent_t e : comm_marks)
+            if (e) (void)hipEventDestroy(e);
         if (comm) comm_release();
         if (comm_st_host) (void)hipHostFree(comm_st_host);
         if (tree_ev) (void)hipEventDestroy(tree_ev);
@@ -1763,8 +1766,16 @@ const RcclApi& rccl() {
     static const RcclApi api = [] {
         RcclApi a;
         void* h = nullptr;
-        for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
-            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        // test hook: MASTIC_RCCL_LIB names the library to bind instead (the
+        // shared-memory stand-in of tests/host/fake_rccl.cpp, which lets several
+        // processes on one GPU form a communicator); no fallback to RCCL
+        const char* hook = getenv("MASTIC_RCCL_LIB");
+        if (hook && *hook) {
+            h = dlopen(hook, RTLD_NOW | RTLD_LOCAL);
+        } else {
+            for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
+                if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        }
         if (!h) {
             const char* e = dlerror();
             a.why = e ? e : "librccl.so.1 not found";
@@ -1812,6 +1823,22 @@ void mastic_ctx::comm_release() {
 // Abort the ctx's communicator after a failed or timed-out RCCL step: its
 // kernels see the abort flag and exit, the ctx keeps comm_broken so later
 // collective calls fail instead of silently folding as world 1.
+// MASTIC_TRACE_COMM: mark step i of the agreement round on the ctx's stream;
+// a timed-out wait reports which marks the stream has passed.
+static void comm_mark(mastic_ctx* c, int i) {
+    if (!trace_comm()) return;
+    if (!c->comm_marks[i] && hipEventCreateWithFlags(&c->comm_marks[i], hipEventDisableTiming) != hipSuccess) return;
+    (void)hipEventRecord(c->comm_marks[i], c->stream);
+}
+static void comm_marks_report(mastic_ctx* c) {
+    if (!trace_comm()) return;
+    for (int i = 0; i < 3; i++)
+        if (c->comm_marks[i])
+            fprintf(stderr, "[mastic comm]   mark %d (%s): %s\n", i,
+                    (const char*[]){"status uploaded", "status all-gather queued", "status download queued"}[i],
+                    hipEventQuery(c->comm_marks[i]) == hipSuccess ? "passed" : "not passed");
+}
+
 static int comm_abort(mastic_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -1859,9 +1886,11 @@ static int comm_wait(mastic_ctx* c, const char* what) {
         ncclResult_t st = ncclSuccess;
         if (rccl().CommGetAsyncError(c->comm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
             return comm_abort(c, MASTIC_EHIP, "RCCL %s: %s", what, rccl().GetErrorString(st));
-        if (now_ms() - t0 > c->comm_timeout_ms)
+        if (now_ms() - t0 > c->comm_timeout_ms) {
+            comm_marks_report(c);
             return comm_abort(c, MASTIC_ETIMEDOUT, "%s: a peer rank did not join within %d ms", what,
                               c->comm_timeout_ms);
+        }
         if (spin < 2000)
             std::this_thread::yield();
         else
@@ -1906,9 +1935,11 @@ static int comm_agree(mastic_ctx* c, int local_rc, uint32_t op, size_t n_local, 
         return comm_abort(c, local_rc ? local_rc : MASTIC_EHIP, "%s: status upload: %s", comm_op_name(op),
                           hipGetErrorString(e));
     }
+    comm_mark(c, 0);
     int rc = comm_settle(c, rccl().AllGather(d, d + sizeof(CommStatus), sizeof(CommStatus), ncclUint8, c->comm,
                                              c->stream), "status all-gather");
     if (rc) return local_rc ? local_rc : rc;
+    comm_mark(c, 1);
     e = hipMemcpyAsync(h + 1, d + sizeof(CommStatus), sizeof(CommStatus) * (size_t)c->comm_n, hipMemcpyDeviceToHost,
                        c->stream);
     if (e != hipSuccess) {
@@ -1916,6 +1947,7 @@ static int comm_agree(mastic_ctx* c, int local_rc, uint32_t op, size_t n_local, 
         return comm_abort(c, local_rc ? local_rc : MASTIC_EHIP, "%s: status download: %s", comm_op_name(op),
                           hipGetErrorString(e));
     }
+    comm_mark(c, 2);
     rc = comm_wait(c, "status all-gather");
     if (rc) return local_rc ? local_rc : rc;
     const CommVerdict v = comm_decide(h + 1, c->comm_n, op, n_local, n_elems);
@@ -1975,6 +2007,17 @@ static int allgather_fold_impl(mastic_ctx* c, const uint32_t* local, size_t n_lo
 // fold, the copy out) done, bounded by the timeout when RCCL is in it.
 static int comm_finish(mastic_ctx* c, uint32_t op) {
     if (c->comm) return comm_wait(c, comm_op_name(op));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// The merged share to the caller's host buffer, AFTER comm_finish: a copy to
+// pageable memory is synchronous, so queued behind a data all-gather that a
+// dead peer never completes it would block this thread past every bound
+// (found by tests/test_gpu_comm_nrank.py: a peer lost between the agreement
+// round and the data all-gather).
+static int comm_copy_out(mastic_ctx* c, void* host_out, size_t bytes) {
+    HIPCHK(c, hipMemcpyAsync(host_out, c->comm_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -2137,9 +2180,9 @@ extern "C" int mastic_merge_host(mastic_ctx* c, const uint8_t* host_local, size_
     rc = comm_agree(c, rc, COMM_MERGE_HOST, n_local, n_elems);
     if (rc || n_elems == 0) return rc;
     rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
+    if (!rc) rc = comm_finish(c, COMM_MERGE_HOST);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(host_out, c->comm_out.p, n_elems * ebytes, hipMemcpyDeviceToHost, c->stream));
-    return comm_finish(c, COMM_MERGE_HOST);
+    return comm_copy_out(c, host_out, n_elems * ebytes);
 }
 
 extern "C" int mastic_aggregate_merged(mastic_ctx* c, uint32_t agg_mask, const uint8_t* valid, size_t n_elems,
@@ -2178,9 +2221,9 @@ extern "C" int mastic_aggregate_merged(mastic_ctx* c, uint32_t agg_mask, const u
     rc = comm_agree(c, rc, COMM_AGGREGATE_MERGED, n_local, n_elems);
     if (rc || n_elems == 0) return rc;
     rc = allgather_fold_impl(c, c->comm_local.as<uint32_t>(), n_local, n_elems, c->comm_out.as<uint32_t>());
+    if (!rc) rc = comm_finish(c, COMM_AGGREGATE_MERGED);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(agg_out, c->comm_out.p, n_elems * ebytes, hipMemcpyDeviceToHost, c->stream));
-    return comm_finish(c, COMM_AGGREGATE_MERGED);
+    return comm_copy_out(c, agg_out, n_elems * ebytes);
 }
 
 // Eval-proof Merkle tree (proof-aggregation mode, kernels.hpp k_proof_tree_*)
