@@ -341,9 +341,12 @@ def comm_record(dist, world, rank, lib_comm, m=None, desc=None):
     devs = [None] * world
     dist.all_gather_object(devs, desc)
     if lib_comm:
-        return {"backend": "rccl", "nranks": int(m.comm_info()[0]), "devices": devs,
+        stand_in = os.environ.get("MASTIC_RCCL_LIB")  # the library's test hook (tests/host/fake_rccl.cpp)
+        return {"backend": "rccl-stand-in" if stand_in else "rccl", "nranks": int(m.comm_info()[0]), "devices": devs,
                 "path": "library-owned RCCL communicator: mastic_aggregate_merged / mastic_allgather_fold "
-                        "(agreement round, ncclAllGather, GF(p) fold on the GPU)"}
+                        "(agreement round, ncclAllGather, GF(p) fold on the GPU)"
+                        + (" -- transport: %s (MASTIC_RCCL_LIB rehearsal, ranks sharing one GPU)" % stand_in
+                           if stand_in else "")}
     return {"backend": "gloo-rehearsal", "nranks": world, "devices": devs,
             "path": "MASTIC_BENCH_BACKEND=gloo: host copies all-gathered over gloo, GF(p) fold on the GPU "
                     "(ranks sharing one GPU)"}

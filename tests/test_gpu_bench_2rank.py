@@ -37,6 +37,36 @@ def test_bench_two_ranks_on_one_gpu():
         assert [x["rank"] for x in c["devices"]] == [0, 1]
 
 
+def test_bench_two_ranks_through_the_library_comm_on_one_gpu():
+    """`--gpus 2` on one GPU with the library's own communicator path (not the
+    gloo merge): the MASTIC_RCCL_LIB test hook binds the shared-memory RCCL
+    stand-in (tests/host/fake_rccl.cpp), so bench.py's lib_comm_init, the C2
+    steps' and the full job's mastic_allgather_fold and the north_star sweep's
+    CommMerge (mastic_aggregate_merged per level) run at two ranks exactly as
+    on the driver's node; the line says which transport carried them."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fake = os.path.join(ROOT, "tests", "host", "_build", "libfake_rccl.so")
+    assert os.path.exists(fake), "run __graft_entry__.build() first"
+    env = dict(os.environ, MASTIC_BENCH_DEVICE="0", MASTIC_RCCL_LIB=fake)
+    env.pop("MASTIC_BENCH_BACKEND", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--reports", "1024", "--total-reports", "2048", "--north-star-reports", "16384", "--cpu-baseline", "0",
+           "--standalone", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["full_job"]["job_reports"] == 4096 and "mastic_allgather_fold" in d["full_job"]["what"]
+    ns = d["north_star"]
+    assert "error" not in ns, ns
+    assert ns["n_gpus"] == 2 and ns["job_reports"] == 16384 and ns["heavy_hitters_equal_plaintext"] is True
+    for c in (d["comm"], ns["comm"]):
+        assert c["backend"] == "rccl-stand-in" and c["nranks"] == 2
+        assert [x["rank"] for x in c["devices"]] == [0, 1]
+
+
 def _run_bench(args, timeout=500):
     env = dict(os.environ, MASTIC_BENCH_BACKEND="gloo", MASTIC_BENCH_DEVICE="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
