@@ -95,7 +95,7 @@ def _worker(rank, world, N, thresh, fake, idq, q):
         # (plus the library's high-priority sponge streams): in 5 of 8 runs one
         # rank's stream stalled after a cross-stream event wait, right after its
         # status all-gather (its peers then timed out and aborted, as designed);
-        # with one hardware queue per process 4 of 4 runs passed.  Deployment
+        # with one hardware queue per process 6 of 6 runs passed.  Deployment
         # is one process per GPU; the rehearsal gives each rank one queue.
         os.environ["GPU_MAX_HW_QUEUES"] = "1"
     import torch
