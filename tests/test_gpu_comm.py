@@ -4,9 +4,10 @@ mastic_allgather_fold, mastic_merge_host, mastic_aggregate_merged; SURVEY.md
 ncclCommInitRank with one rank, the all-gather on the ctx's stream, then the
 GF(p) fold.  Every result equals the single-GPU forms (mastic_aggregate,
 mastic_fold_shares) and the field sum (Mastic.merge, poc/mastic.py:390-397).
-RCCL refuses two ranks on one device, so world > 1 runs on the driver's
-8-GPU node; tests/test_multirank_cpu.py and tests/test_split_cpu.py cover the
-multi-rank host logic over gloo."""
+RCCL refuses two ranks on one device, so the library's world > 1 path runs
+on one GPU through a shared-memory RCCL stand-in (tests/test_gpu_comm_nrank.py)
+and with real RCCL on the driver's 8-GPU node; tests/test_multirank_cpu.py and
+tests/test_split_cpu.py cover the multi-rank host logic over gloo."""
 import random
 
 import numpy as np
