@@ -29,7 +29,8 @@ from conftest import PKG_ROOT, ROOT
 pytestmark = pytest.mark.gpu
 
 BITS, SEED, TIMEOUT_MS = 10, 91, 4000
-CASES = [(2, 600, 12), (3, 601, 12), (3, 450, 9)]
+# (ranks, reports, threshold); the last: rank 0 holds no reports (CommMerge.total(have_results=False))
+CASES = [(2, 600, 12), (3, 601, 12), (3, 450, 9), (3, 2, 1)]
 
 
 def _fake_rccl():
@@ -95,7 +96,7 @@ def _worker(rank, world, N, thresh, fake, idq, q):
         # (plus the library's high-priority sponge streams): in 5 of 8 runs one
         # rank's stream stalled after a cross-stream event wait, right after its
         # status all-gather (its peers then timed out and aborted, as designed);
-        # with one hardware queue per process 6 of 6 runs passed.  Deployment
+        # with one hardware queue per process 9 of 9 runs passed.  Deployment
         # is one process per GPU; the rehearsal gives each rank one queue.
         os.environ["GPU_MAX_HW_QUEUES"] = "1"
     import torch
@@ -139,15 +140,20 @@ def _worker(rank, world, N, thresh, fake, idq, q):
     # 2. the split sweep (CommMerge per level) and one aggregate_merged step
     ctx = b"n-ranks"
     lo, hi = N * rank // world, N * (rank + 1) // world
-    reps = _reports(m, ctx, N, lo, hi)
+    reps = _reports(m, ctx, N, lo, hi) if hi > lo else []  # a rank without reports
     (_a, _w, _n, _r, vk, pool) = _population(N)
     trace = []
     out["hh"] = compute_heavy_hitters(m, ctx, {"default": thresh}, reps, verify_key=vk, trace=trace,
                                       merge=CommMerge(m))
     out["trace"] = [(t.level, t.prefixes, t.agg_result) for t in trace]
     ap = _agg_param(pool)
-    m.prep_init_device(reps, vk, ctx, 0, m.encode_agg_param(ap))
-    out["agg"] = m.aggregate_merged((0,), len(ap[1]) * (1 + m.OUTPUT_LEN))
+    n_ap = len(ap[1]) * (1 + m.OUTPUT_LEN)
+    if hi > lo:
+        m.prep_init_device(reps, vk, ctx, 0, m.encode_agg_param(ap))
+        out["agg"] = m.aggregate_merged((0,), n_ap)
+    else:
+        out["agg"] = m.aggregate_merged((0,), n_ap, zeros=True)  # agg_init's zeros, same collective
+    out["n_reports"] = hi - lo
     say("sweep and step done")
 
     # 3. calls that disagree on the geometry
@@ -181,7 +187,7 @@ def _worker(rank, world, N, thresh, fake, idq, q):
     q.put((rank, out))
 
 
-@pytest.mark.parametrize("world,N,thresh", CASES, ids=["2x600", "3x601", "3x450"])
+@pytest.mark.parametrize("world,N,thresh", CASES, ids=["2x600", "3x601", "3x450", "3x2-empty-rank"])
 def test_n_ranks_on_one_gpu_through_the_library_comm(world, N, thresh):
     import torch
     if not torch.cuda.is_available():
@@ -231,6 +237,9 @@ def test_n_ranks_on_one_gpu_through_the_library_comm(world, N, thresh):
     enc = m.encode_agg_param(ap)
     m.prep_init_device(reps, vk, ctx, 0, enc)
     want_agg = m.aggregate_device(0, enc, raw=True)
+    assert sum(got[r]["n_reports"] for r in range(world)) == N
+    if N < world:
+        assert got[0]["n_reports"] == 0, "the case must give rank 0 no reports"
     for r in range(world):
         assert got[r]["hh"] == hh
         assert got[r]["trace"] == [(t.level, t.prefixes, t.agg_result) for t in trace]
