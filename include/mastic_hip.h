@@ -204,7 +204,12 @@ int mastic_fold_shares(mastic_ctx* ctx, const void* dev_shares, size_t n_shares,
  * stays on a library thread, which releases the communicator if the peers
  * ever arrive); a timed-out collective aborts the communicator, and later
  * collective calls fail with MASTIC_EHIP (never a silent world-1 merge) until
- * mastic_comm_destroy and a new mastic_comm_init. */
+ * mastic_comm_destroy and a new mastic_comm_init.  Host output buffers
+ * (host_out, agg_out) are written only after the bounded wait succeeded; on
+ * any error they are left untouched.  Test hook: the environment variable
+ * MASTIC_RCCL_LIB names a library to bind instead of librccl (no fallback);
+ * tests/host/fake_rccl.cpp is a shared-memory stand-in that lets several
+ * processes on one GPU form a communicator. */
 #define MASTIC_COMM_ID_BYTES 128
 #define MASTIC_COMM_TIMEOUT_MS 120000 /* mastic_comm_init's bound on every communicator wait */
 int mastic_comm_unique_id(uint8_t id_out[MASTIC_COMM_ID_BYTES]);
