@@ -95,10 +95,11 @@ def _worker(rank, world, N, thresh, fake, idq, q):
         # Three processes on one GPU with HIP's default 4 hardware queues each
         # (plus the library's high-priority sponge streams): in 5 of 8 runs one
         # rank's stream stalled after a cross-stream event wait, right after its
-        # status all-gather (its peers then timed out and aborted, as designed);
-        # with one hardware queue per process 9 of 9 runs passed.  Deployment
-        # is one process per GPU; the rehearsal gives each rank one queue.
-        os.environ["GPU_MAX_HW_QUEUES"] = "1"
+        # status all-gather (its peers then timed out and aborted, as designed),
+        # and 2 of 3 with SDMA copies off (HSA_ENABLE_SDMA=0); with one hardware
+        # queue per process 9 of 9 runs passed.  Deployment is one process per
+        # GPU; the rehearsal gives each rank one queue.
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("NRANK_HW_QUEUES", "1")  # (override: experiments)
     import torch
     torch.cuda.set_device(0)
     say("torch up")
